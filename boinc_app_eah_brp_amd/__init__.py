@@ -1,0 +1,54 @@
+"""MI355X-native Einstein@Home binary radio pulsar (BRP) search.
+
+A from-scratch re-design of the capabilities of boinc-app-eah-brp for AMD
+Instinct MI355X (gfx950): the per-template pipeline (time-domain resampling,
+3*2^n-point real FFT + power spectrum, 16-harmonic summing, candidate
+selection) runs as hand-written HIP kernels, templates are batched in HBM and
+replayed through HIP graphs, and template banks are sharded over GPUs with
+RCCL all-gathers of the candidate tables.
+
+Layout:
+  models/    search pipelines (GPU search, CPU golden model, numpy oracle)
+  ops/       device operations (power spectrum, harmonic sums, whitening)
+  parallel/  multi-GPU sharding over torch.distributed (RCCL / gloo)
+  utils/     file formats, synthetic data, statistics
+The native code lives in csrc/ and is built in-tree by `_build.py`.
+"""
+from __future__ import annotations
+
+import importlib
+import os
+import sys
+
+__version__ = "0.1.0"
+
+_native = None
+
+
+def native():
+    """Return the compiled extension module, building it on first use if needed."""
+    global _native
+    if _native is not None:
+        return _native
+    # torch (when present) must load its HIP runtime first so both share one copy
+    if "torch" not in sys.modules:
+        try:
+            import torch  # noqa: F401
+        except Exception:  # pragma: no cover - torch is optional for CPU-only use
+            pass
+    try:
+        _native = importlib.import_module("._brp", __name__)
+    except ImportError:
+        if os.environ.get("BRP_NO_AUTOBUILD"):
+            raise
+        from . import _build
+
+        _build.build(verbose=False)
+        _native = importlib.import_module("._brp", __name__)
+    return _native
+
+
+def __getattr__(name):  # lazy access: boinc_app_eah_brp_amd.models etc.
+    if name in ("models", "ops", "parallel", "utils"):
+        return importlib.import_module("." + name, __name__)
+    raise AttributeError(name)

@@ -1,0 +1,155 @@
+"""In-tree native build of the framework (no setup.py / JIT cache).
+
+Products (all git-ignored, shipped to GPU boxes with the repo snapshot):
+  boinc_app_eah_brp_amd/_brp<EXT_SUFFIX>   Python extension (pybind11)
+  bin/einsteinbinary_mi355x                BOINC application (C++ main)
+  build/obj/*.o                            object cache
+
+Device code is compiled for gfx950 only with hipcc; host-only C++ with
+amdclang++. Run:  python -m boinc_app_eah_brp_amd._build [--force] [-j N]
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import os
+import subprocess
+import sys
+import sysconfig
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+CSRC = ROOT / "csrc"
+OBJ = ROOT / "build" / "obj"
+PKG = ROOT / "boinc_app_eah_brp_amd"
+BIN = ROOT / "bin"
+ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
+HIPCC = str(ROCM / "bin" / "hipcc")
+CLANG = str(ROCM / "llvm" / "bin" / "clang++")
+ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0]
+
+HOST_SRCS = [
+    "core/log.cpp", "core/io.cpp", "core/stats.cpp", "core/gsl_compat.cpp", "core/rngmed.cpp",
+    "core/search_core.cpp", "core/cpu_fft.cpp", "core/cpu_backend.cpp",
+    "boinc/boinc_shim.cpp", "boinc/ipc.cpp",
+    "engine/cpu_engine.cpp", "engine/hip_engine.cpp",
+    "app/search.cpp", "app/cli.cpp",
+]
+DEVICE_SRCS = [
+    "hip/fft_passes.hip", "hip/harmonic_sum.hip", "hip/resample.hip", "hip/whiten.hip",
+]
+BINDING_SRCS = ["bindings/pybind.cpp"]
+APP_MAIN = "app/main.cpp"
+
+
+def ext_suffix() -> str:
+    return sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+
+
+def extension_path() -> Path:
+    return PKG / f"_brp{ext_suffix()}"
+
+
+def app_path() -> Path:
+    return BIN / "einsteinbinary_mi355x"
+
+
+def git_id() -> str:
+    try:
+        return subprocess.check_output(["git", "-C", str(ROOT), "rev-parse", "HEAD"], stderr=subprocess.DEVNULL,
+                                       text=True).strip()
+    except Exception:
+        return "unknown"
+
+
+def _common_flags() -> list[str]:
+    return ["-O3", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-function", "-Wno-unknown-pragmas",
+            "-D__HIP_PLATFORM_AMD__", f"-I{ROCM / 'include'}", f'-DBRP_GIT_ID="{git_id()[:40]}"']
+
+
+def _headers_mtime() -> float:
+    return max(p.stat().st_mtime for p in CSRC.rglob("*.hpp"))
+
+
+def _needs(obj: Path, src: Path, hdr_mtime: float, force: bool) -> bool:
+    if force or not obj.exists():
+        return True
+    return obj.stat().st_mtime < max(src.stat().st_mtime, hdr_mtime)
+
+
+def _compile(src_rel: str, force: bool, hdr_mtime: float) -> tuple[str, Path]:
+    src = CSRC / src_rel
+    obj = OBJ / (src_rel.replace("/", "__") + ".o")
+    if not _needs(obj, src, hdr_mtime, force):
+        return "cached", obj
+    obj.parent.mkdir(parents=True, exist_ok=True)
+    if src.suffix == ".hip":
+        cmd = [HIPCC, f"--offload-arch={ARCH}", *_common_flags(), "-munsafe-fp-atomics", "-c", str(src), "-o", str(obj)]
+    else:
+        flags = _common_flags()
+        if src_rel.startswith("bindings/"):
+            import pybind11
+            flags += [f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}",
+                      "-fvisibility=hidden"]
+        cmd = [CLANG, *flags, "-c", str(src), "-o", str(obj)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"compile failed: {src_rel}\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    return "built", obj
+
+
+def _link(objs: list[Path], out: Path, shared: bool) -> None:
+    out.parent.mkdir(parents=True, exist_ok=True)
+    tmp = out.with_name(out.name + ".tmp")
+    cmd = [HIPCC, f"--offload-arch={ARCH}", *[str(o) for o in objs], "-o", str(tmp),
+           f"-L{ROCM / 'lib'}", "-lamdhip64", "-lz", "-lpthread"]
+    if shared:
+        cmd.insert(1, "-shared")
+    else:
+        cmd += [f"-Wl,-rpath,{ROCM / 'lib'}"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed: {out}\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    os.replace(tmp, out)
+
+
+def build(force: bool = False, jobs: int | None = None, verbose: bool = True) -> dict:
+    jobs = jobs or min(16, os.cpu_count() or 4)
+    hdr = _headers_mtime()
+    srcs = HOST_SRCS + DEVICE_SRCS + BINDING_SRCS + [APP_MAIN]
+    results = {}
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        futs = {ex.submit(_compile, s, force, hdr): s for s in srcs}
+        for f in cf.as_completed(futs):
+            status, obj = f.result()
+            results[futs[f]] = obj
+            if verbose and status == "built":
+                print(f"[build] {futs[f]}", flush=True)
+    core = [results[s] for s in HOST_SRCS + DEVICE_SRCS]
+    ext = extension_path()
+    ext_objs = core + [results[s] for s in BINDING_SRCS]
+    if force or not ext.exists() or ext.stat().st_mtime < max(o.stat().st_mtime for o in ext_objs):
+        _link(ext_objs, ext, shared=True)
+        if verbose:
+            print(f"[build] linked {ext.relative_to(ROOT)}", flush=True)
+    app = app_path()
+    app_objs = core + [results[APP_MAIN]]
+    if force or not app.exists() or app.stat().st_mtime < max(o.stat().st_mtime for o in app_objs):
+        _link(app_objs, app, shared=False)
+        if verbose:
+            print(f"[build] linked {app.relative_to(ROOT)}", flush=True)
+    return {"extension": str(ext), "app": str(app)}
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-j", "--jobs", type=int, default=None)
+    a = ap.parse_args(argv)
+    out = build(force=a.force, jobs=a.jobs)
+    print(out)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,402 @@
+#include "search.hpp"
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cmath>
+#include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <set>
+#include <thread>
+
+#include "../boinc/boinc_shim.hpp"
+#include "../boinc/ipc.hpp"
+#include "../core/errors.hpp"
+#include "../core/io.hpp"
+#include "../core/log.hpp"
+#include "../core/stats.hpp"
+
+#ifndef BRP_GIT_ID
+#define BRP_GIT_ID "unknown"
+#endif
+
+namespace brp {
+
+namespace {
+
+double now_s() {
+  using namespace std::chrono;
+  return duration<double>(steady_clock::now().time_since_epoch()).count();
+}
+
+// RA/DEC (hhmmss.s / ddmmss.s) to radians for the screensaver (demod_binary.c:745-771)
+void sky_position(const DDHeader& h, SearchInfo& info) {
+  float hrs = std::floor(h.RA / 10000.0);
+  float min = std::floor((h.RA - 10000.0 * hrs) / 100.0);
+  float sec = h.RA - 10000.0 * hrs - 100.0 * min;
+  info.skypos_rac = M_PI * (hrs / 12.0 + min / 720.0 + sec / 43200.0);
+  if (h.DEC < 0.0) {
+    hrs = std::floor(-h.DEC / 10000.0);
+    min = std::floor(-(h.DEC + 10000.0 * hrs) / 100.0);
+    sec = -(h.DEC + 10000.0 * hrs + 100.0 * min);
+    info.skypos_dec = -M_PI * (hrs / 180.0 + min / 10800.0 + sec / 648000.0);
+  } else {
+    hrs = std::floor(h.DEC / 10000.0);
+    min = std::floor((h.DEC - 10000.0 * hrs) / 100.0);
+    sec = h.DEC - 10000.0 * hrs - 100.0 * min;
+    info.skypos_dec = M_PI * (hrs / 180.0 + min / 10800.0 + sec / 648000.0);
+  }
+  info.dispersion_measure = h.DM;
+}
+
+void log_header(const DDHeader& h) {
+  log_message(LOG_INFO, true, "Header contents:\n");
+  log_message(LOG_INFO, false, "Original WAPP file: %s\n", h.originalfile);
+  log_message(LOG_INFO, false, "Sample time in microseconds: %g\n", h.tsample);
+  log_message(LOG_INFO, false, "Observation time in seconds: %.8g\n", h.tobs);
+  log_message(LOG_INFO, false, "Time stamp (MJD): %.17g\n", h.timestamp);
+  log_message(LOG_INFO, false, "Number of samples/record: %d\n", h.smprec);
+  log_message(LOG_INFO, false, "Center freq in MHz: %.10g\n", h.fcenter);
+  log_message(LOG_INFO, false, "Channel band in MHz: %.9g\n", h.fchan);
+  log_message(LOG_INFO, false, "Number of channels/record: %d\n", h.nchan);
+  log_message(LOG_INFO, false, "Nifs: %d\n", h.nifs);
+  log_message(LOG_INFO, false, "RA (J2000): %.12g\n", h.RA);
+  log_message(LOG_INFO, false, "DEC (J2000): %.12g\n", h.DEC);
+  log_message(LOG_INFO, false, "Galactic l: %.7g\n", h.gal_l);
+  log_message(LOG_INFO, false, "Galactic b: %.7g\n", h.gal_b);
+  log_message(LOG_INFO, false, "Name: %s\n", h.name);
+  log_message(LOG_INFO, false, "Lagformat: %d\n", h.lagformat);
+  log_message(LOG_INFO, false, "Sum: %d\n", h.sum);
+  log_message(LOG_INFO, false, "Level: %d\n", h.level);
+  log_message(LOG_INFO, false, "AZ at start: %.9g\n", h.AZstart);
+  log_message(LOG_INFO, false, "ZA at start: %.9g\n", h.ZAstart);
+  log_message(LOG_INFO, false, "AST at start: %.9g\n", h.ASTstart);
+  log_message(LOG_INFO, false, "LST at start: %.9g\n", h.LSTstart);
+  log_message(LOG_INFO, false, "Project ID: %s\n", h.proj_id);
+  log_message(LOG_INFO, false, "Observers: %s\n", h.observers);
+  log_message(LOG_INFO, false, "File size (bytes): %d\n", h.filesize);
+  log_message(LOG_INFO, false, "Data size (bytes): %d\n", h.datasize);
+  log_message(LOG_INFO, false, "Number of samples: %d\n", h.nsamples);
+  log_message(LOG_INFO, false, "Trial dispersion measure: %g cm^-3 pc\n", h.DM);
+  log_message(LOG_INFO, false, "Scale factor: %g\n", h.scale);
+}
+
+// Results of one dispatched batch, applied in template order by the driver.
+struct BatchResult {
+  uint32_t first = 0;
+  int rc = 0;
+  std::vector<TemplateCands> cands;
+};
+
+}  // namespace
+
+int finalize_output(const SearchOptions& opt, const SearchGeometry& g, uint32_t n_done, CandidateTable& table,
+                    const std::string& exec_name) {
+  if (!opt.checkpointfile.empty()) {
+    Checkpoint cp;
+    std::memset(&cp.header, 0, sizeof(cp.header));
+    cp.header.n_template = n_done;
+    std::snprintf(cp.header.originalfile, sizeof(cp.header.originalfile), "%s", opt.inputfile.c_str());
+    std::memcpy(cp.cands, table.data(), sizeof(cp.cands));
+    int rc = write_checkpoint(opt.checkpointfile, cp);
+    if (rc) return rc;
+  }
+  if (opt.outputfile.empty()) return 0;
+  ResultHeaderInfo info;
+  info.write_header = std::getenv("BRP_NO_RESULT_HEADER") == nullptr;
+  const boinc::InitData& id = boinc::init_data();
+  if (id.valid) {
+    info.user_id = id.userid;
+    info.user_name = id.user_name;
+    info.host_id = id.hostid;
+    info.host_cpid = id.host_cpid;
+  } else if (info.write_header) {
+    log_message(LOG_WARN, true, "User/host details unavailable...\n");
+  }
+  std::string ex = exec_name;
+  const size_t slash = ex.find_last_of("\\/");
+  if (slash != std::string::npos) ex = ex.substr(slash + 1);
+  info.exec_name = ex;
+  info.git_id = BRP_GIT_ID;
+  info.boinc_rev = "standalone-shim";
+  CPCand cands[kCandTotal];
+  std::memcpy(cands, table.data(), sizeof(cands));
+  return write_results(opt.outputfile, cands, g.t_obs_d, info);
+}
+
+int run_search(const SearchOptions& opt, const SearchControl& ctl, SearchResult& res) {
+  const double t_start = now_s();
+  res = SearchResult();
+  log_message(LOG_INFO, true, "Starting data processing...\n");
+
+  // template bank (counted up front like the reference, demod_binary.c:506-544)
+  TemplateBank bank;
+  int rc = read_template_bank(opt.templatebank, bank);
+  if (rc) return rc;
+  const uint32_t total = static_cast<uint32_t>(bank.size());
+  res.templates_total = total;
+  log_message(LOG_DEBUG, true, "Total amount of templates: %u\n", total);
+
+  // checkpoint restore (demod_binary.c:546-652)
+  CandidateTable& table = res.table;
+  uint32_t counter = 0;
+  if (ctl.use_checkpoint && !opt.checkpointfile.empty()) {
+    Checkpoint cp;
+    bool exists = false;
+    rc = read_checkpoint(opt.checkpointfile, cp, exists);
+    if (rc) return rc;
+    if (!exists) {
+      log_message(LOG_INFO, true, "Checkpoint file unavailable: %s.\n", opt.checkpointfile.c_str());
+      log_message(LOG_INFO, false, "Starting from scratch...\n");
+      if (opt.inputfile.size() >= static_cast<size_t>(kFnLength)) {
+        log_message(LOG_ERROR, true, "Couldn't write input file %s name to checkpoint header.\n",
+                    opt.inputfile.c_str());
+        return RADPUL_EFILE;
+      }
+    } else {
+      if (cp.header.n_template == total) {
+        log_message(LOG_INFO, true, "Thank you but this work unit has already been processed completely...\n");
+      } else if (cp.header.n_template < total) {
+        log_message(LOG_INFO, true, "Continuing work on %s at template no. %u\n", cp.header.originalfile,
+                    cp.header.n_template);
+      } else {
+        log_message(LOG_ERROR, true,
+                    "Header checkpoint file %s contains inconsistent information about number of templates done "
+                    "(%u > %u).\n",
+                    opt.checkpointfile.c_str(), cp.header.n_template, total);
+        return RADPUL_EFILE;
+      }
+      cp.header.originalfile[kFnLength - 1] = 0;
+      if (opt.inputfile != cp.header.originalfile) {
+        log_message(LOG_ERROR, true, "Input file on command line %s doesn't agree with input file %s from checkpoint header.\n",
+                    opt.inputfile.c_str(), cp.header.originalfile);
+        return RADPUL_EFILE;
+      }
+      std::memcpy(table.data(), cp.cands, sizeof(cp.cands));
+      counter = cp.header.n_template;
+      if (opt.debug) {
+        log_message(LOG_DEBUG, true, "Candidates found so far:\n");
+        for (int i = 0; i < kCandTotal; ++i) {
+          const CPCand& c = table.data()[i];
+          log_message(LOG_DEBUG, false, "%u %6.12f %6.12f %6.12f %6.12f %u\n", c.f0, c.power, c.P_b, c.tau, c.Psi,
+                      c.n_harm);
+        }
+      }
+    }
+  }
+
+  // work unit
+  WorkUnit wu;
+  rc = read_work_unit(opt.inputfile, wu);
+  if (rc) return rc;
+  if (opt.debug) log_header(wu.header);
+  SearchInfo info;
+  sky_position(wu.header, info);
+  SearchGeometry& g = res.geom;
+  rc = derive_geometry(wu.header, opt, g);
+  if (rc) return rc;
+  std::vector<ZapRange> zaps;
+  if (opt.white) {
+    if (opt.zaplistfile.empty()) {
+      log_message(LOG_ERROR, true, "Whitening requested but no zaplist file given (-l).\n");
+      return RADPUL_EFILE;
+    }
+    rc = read_zaplist(opt.zaplistfile, zaps);
+    if (rc) return rc;
+  }
+  if (opt.debug) {
+    log_message(LOG_INFO, true, "Derived global search parameters:\n");
+    log_message(LOG_INFO, false, "f_A probability = %g\n", opt.fA);
+    log_message(LOG_INFO, false, "single bin prob(P_noise > P_thr) = %g\n", g.prob);
+    const char* names[5] = {"thr1", "thr2", "thr4", "thr8", "thr16"};
+    for (int h = 0; h < 5; ++h)
+      log_message(LOG_INFO, false, "%s = %g\n", names[h], 0.5 * chisq_Qinv_even(g.prob, 1 << h));
+  }
+
+  // backends: one per device, driven from this process
+  const uint32_t begin = std::max(counter, ctl.begin);
+  const uint32_t end = (ctl.end == 0 || ctl.end > total) ? total : ctl.end;
+  std::vector<std::unique_ptr<Backend>> backends;
+  const int ngpu = opt.use_cpu ? 1 : std::max(1, ctl.gpus);
+  boinc::begin_critical_section();
+  for (int k = 0; k < ngpu; ++k) {
+    std::unique_ptr<Backend> b;
+    if (opt.use_cpu) {
+      b = make_cpu_backend();
+    } else {
+      int dev = opt.device;
+      if (!ctl.devices.empty()) dev = ctl.devices[k % ctl.devices.size()];
+      else if (ngpu > 1) dev = k;
+      else if (dev < 0 && boinc::init_data().gpu_device_num >= 0) dev = boinc::init_data().gpu_device_num;
+      int err = 0;
+      b = make_hip_backend(dev, opt.batch, &err);
+      if (!b) return err ? err : RADPUL_HIP_DEVICE_FIND;
+    }
+    backends.push_back(std::move(b));
+  }
+  std::vector<float> series = wu.samples;
+  if (begin < end) {
+    rc = backends[0]->setup(g, opt, series, zaps);
+    if (rc) return rc;
+    SearchOptions opt_nw = opt;
+    opt_nw.white = false;
+    for (size_t k = 1; k < backends.size(); ++k) {
+      rc = backends[k]->setup(g, opt_nw, series, zaps);
+      if (rc) return rc;
+    }
+  }
+  boinc::end_critical_section();
+  res.t_setup = now_s() - t_start;
+
+  // template loop: batches dispatched to the devices, results applied in
+  // template order so the candidate table evolves exactly as in the
+  // sequential reference loop (demod_binary.c:1180-1443)
+  const double t_loop = now_s();
+  const int B = std::max(1, backends[0]->preferred_batch());
+  std::vector<TemplateInput> tin(total);
+  for (uint32_t t = 0; t < total; ++t)
+    tin[t] = TemplateInput{static_cast<float>(bank.P[t]), static_cast<float>(bank.tau[t]), static_cast<float>(bank.Psi0[t])};
+
+  std::mutex mu;
+  std::condition_variable cv;
+  std::map<uint32_t, BatchResult> ready;
+  float thr_shared[kNumHarmonicLevels];
+  table.thresholds(g.chi2_thr, thr_shared);
+  std::atomic<uint32_t> next_first{begin};
+  std::atomic<bool> stop{false};
+  auto worker = [&](Backend* be) {
+    for (;;) {
+      if (stop.load()) return;
+      const uint32_t first = next_first.fetch_add(static_cast<uint32_t>(B));
+      if (first >= end) return;
+      const int n = static_cast<int>(std::min<uint32_t>(B, end - first));
+      float thr[kNumHarmonicLevels];
+      {
+        std::lock_guard<std::mutex> lk(mu);
+        std::memcpy(thr, thr_shared, sizeof(thr));
+      }
+      BatchResult br;
+      br.first = first;
+      br.rc = be->process(&tin[first], n, thr, br.cands);
+      {
+        std::lock_guard<std::mutex> lk(mu);
+        ready.emplace(first, std::move(br));
+      }
+      cv.notify_all();
+    }
+  };
+  std::vector<std::thread> threads;
+  for (auto& be : backends) threads.emplace_back(worker, be.get());
+
+  uint32_t applied = begin;
+  rc = 0;
+  std::set<uint32_t> pages;
+  const char* fault = std::getenv("BRP_FAULT");
+  long kill_after = -1;
+  if (fault && std::strncmp(fault, "kill_after_template:", 20) == 0) kill_after = std::atol(fault + 20);
+  bool quit = false;
+  while (applied < end && !quit) {
+    BatchResult br;
+    {
+      std::unique_lock<std::mutex> lk(mu);
+      cv.wait(lk, [&] { return ready.count(applied) > 0; });
+      br = std::move(ready[applied]);
+      ready.erase(applied);
+    }
+    if (br.rc) {
+      rc = br.rc;
+      break;
+    }
+    for (size_t k = 0; k < br.cands.size() && !quit; ++k) {
+      const uint32_t t = br.first + static_cast<uint32_t>(k);
+      const TemplateInput& ti = tin[t];
+      float thrA[kNumHarmonicLevels];
+      table.thresholds(g.chi2_thr, thrA);
+      unsigned char binned[kBinsScreensaver] = {0};
+      for (int h = 0; h < kNumHarmonicLevels; ++h) {
+        const std::vector<BinPower>& lv = br.cands[k].level[h];
+        table.apply_level(h, lv.data(), lv.size(), thrA[h], ti.P, ti.tau, ti.Psi0);
+        pages.clear();
+        for (const BinPower& bp : lv)
+          if (bp.power > thrA[h]) pages.insert(bp.bin >> kLogPsPageSize);
+        res.dirty_pages += pages.size();
+        if (h == 2) {
+          const float powerscale = 100.0f / 255.0f;
+          const float stepscale = static_cast<float>(kBinsScreensaver) / static_cast<float>(g.fundamental_idx_hi);
+          for (const BinPower& bp : lv) {
+            const int bin_ss = static_cast<int>(stepscale * bp.bin);
+            if (bin_ss >= 0 && bin_ss < kBinsScreensaver && bp.power > powerscale * binned[bin_ss])
+              binned[bin_ss] = static_cast<unsigned char>(std::min(bp.power / powerscale, 255.0f));
+          }
+        }
+      }
+      info.orbital_radius = ti.tau;
+      info.orbital_period = ti.P;
+      info.orbital_phase = ti.Psi0;
+      std::memcpy(info.power_spectrum, binned, sizeof(binned));
+      if (ipc::update_due()) ipc::update_shmem(info);
+      ++counter;
+      ++res.templates_run;
+      boinc::fraction_done((counter + 1.0) / total);
+      if (ctl.on_template) ctl.on_template(counter, total);
+      if (ctl.use_checkpoint && !opt.checkpointfile.empty() && boinc::time_to_checkpoint()) {
+        Checkpoint cp;
+        std::memset(&cp.header, 0, sizeof(cp.header));
+        cp.header.n_template = counter;
+        std::snprintf(cp.header.originalfile, sizeof(cp.header.originalfile), "%s", opt.inputfile.c_str());
+        std::memcpy(cp.cands, table.data(), sizeof(cp.cands));
+        rc = write_checkpoint(opt.checkpointfile, cp);
+        if (rc) break;
+        log_message(LOG_INFO, true, "Checkpoint committed!\n");
+        boinc::checkpoint_completed();
+      }
+      if (kill_after >= 0 && counter >= static_cast<uint32_t>(kill_after)) boinc::request_quit();
+      const boinc::Status st = boinc::get_status();
+      if (st.quit_request || st.abort_request || st.no_heartbeat) quit = true;
+    }
+    if (rc) break;
+    applied = br.first + static_cast<uint32_t>(br.cands.size());
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      table.thresholds(g.chi2_thr, thr_shared);
+    }
+  }
+  stop.store(true);
+  for (auto& th : threads) th.join();
+  res.t_templates = now_s() - t_loop;
+  res.templates_done = counter;
+  for (auto& be : backends) {
+    const BackendStats s = be->stats();
+    res.stats.gpu_ms += s.gpu_ms;
+    res.stats.whiten_ms += s.whiten_ms;
+    res.stats.templates += s.templates;
+    res.stats.batches += s.batches;
+    res.stats.overflow_reruns += s.overflow_reruns;
+  }
+  if (rc) return rc;
+  if (quit) {
+    res.interrupted = true;
+    log_message(LOG_WARN, true, "BOINC wants us to quit prematurely or we lost contact! Exiting...\n");
+    res.t_total = now_s() - t_start;
+    return 0;
+  }
+  if (ctl.write_output) {
+    log_message(LOG_DEBUG, true, "Search done!\n");
+    rc = finalize_output(opt, g, counter, table, "einsteinbinary_mi355x");
+    if (rc) return rc;
+  }
+  log_message(LOG_INFO, true,
+              "Statistics: count dirty SumSpec pages %llu (not checkpointed), Page Size %d, fundamental_idx_hi-window_2: %u\n",
+              static_cast<unsigned long long>(res.dirty_pages), 1 << kLogPsPageSize,
+              g.fundamental_idx_hi - g.window_2);
+  res.t_total = now_s() - t_start;
+  log_message(LOG_INFO, true, "Data processing finished successfully!\n");
+  return 0;
+}
+
+}  // namespace brp

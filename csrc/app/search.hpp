@@ -1,0 +1,53 @@
+// The search driver (reference MAIN, demod_binary.c:117-1695).
+#pragma once
+
+#include <cstdint>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "../core/search_core.hpp"
+#include "../engine/backend.hpp"
+
+namespace brp {
+
+struct SearchResult {
+  CandidateTable table;
+  SearchGeometry geom;
+  uint32_t templates_total = 0;
+  uint32_t templates_done = 0;   // including those restored from a checkpoint
+  uint32_t templates_run = 0;    // processed in this call
+  bool interrupted = false;      // quit request: no final checkpoint/output
+  double t_setup = 0, t_templates = 0, t_total = 0;  // seconds
+  uint64_t dirty_pages = 0;
+  BackendStats stats;
+};
+
+struct SearchControl {
+  // restrict to templates [begin, end) of the bank (sharded runs); end=0: all
+  uint32_t begin = 0, end = 0;
+  bool write_output = true;       // result file + final checkpoint
+  bool use_checkpoint = true;
+  int gpus = 1;                   // devices driven by this process (in-order merge)
+  std::vector<int> devices;       // explicit device ids (optional)
+  // called after every template applied (progress hooks / fault injection)
+  std::function<void(uint32_t done, uint32_t total)> on_template;
+};
+
+// Full search of one WU with the options' files. Returns a RADPUL_* code.
+int run_search(const SearchOptions& opt, const SearchControl& ctl, SearchResult& res);
+
+// MAIN-compatible entry: parses the reference command line (short options and
+// the --input_file style long names, demod_binary.c:217-445) plus MI355X
+// extensions (--mi355x-batch N, --mi355x-gpus N, --mi355x-cpu).
+int search_main(int argc, char** argv);
+
+// BOINC wrapper entry (erp_boinc_wrapper.cpp:242-584): getopt_long with the
+// dashed long names, several -i/-o pairs processed as sequential passes.
+int wrapper_main(int argc, char** argv);
+
+// Final stage shared by single and sharded runs: checkpoint + result file.
+int finalize_output(const SearchOptions& opt, const SearchGeometry& g, uint32_t n_done, CandidateTable& table,
+                    const std::string& exec_name);
+
+}  // namespace brp

@@ -1,0 +1,53 @@
+// Compute-backend interface of the search driver (the reference selects its
+// backend at link time: set_up_/run_/tear_down_{resampling,fft,harmonic_summing},
+// demod_binary.c:64-81). Here a backend owns the whole per-WU device state and
+// processes *batches* of templates, returning the above-threshold bins of every
+// template; the driver applies them to the candidate table in template order.
+#pragma once
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../core/io.hpp"
+#include "../core/search_core.hpp"
+
+namespace brp {
+
+struct TemplateInput {
+  float P, tau, Psi0;
+};
+
+struct TemplateCands {
+  std::vector<BinPower> level[kNumHarmonicLevels];  // ascending bins
+};
+
+struct BackendStats {
+  double gpu_ms = 0;         // device time of template batches
+  double whiten_ms = 0;      // device time of the whitening step
+  uint64_t templates = 0;
+  uint64_t batches = 0;
+  uint64_t overflow_reruns = 0;
+};
+
+class Backend {
+ public:
+  virtual ~Backend() = default;
+  virtual const char* name() const = 0;
+  // Per-WU setup: upload the series, whiten/zap it if opt.white (series is
+  // updated in place with the whitened data).
+  virtual int setup(const SearchGeometry& g, const SearchOptions& opt, std::vector<float>& series,
+                    const std::vector<ZapRange>& zaps) = 0;
+  // Process n templates with device thresholds thr (<= the sequential
+  // thresholds of every template in the batch).
+  virtual int process(const TemplateInput* t, int n, const float thr[kNumHarmonicLevels],
+                      std::vector<TemplateCands>& out) = 0;
+  virtual int preferred_batch() const = 0;
+  virtual BackendStats stats() const { return {}; }
+};
+
+std::unique_ptr<Backend> make_cpu_backend();
+// device < 0: auto (BOINC gpu_device_num / first device)
+std::unique_ptr<Backend> make_hip_backend(int device, int batch, int* err);
+
+}  // namespace brp

@@ -1,0 +1,627 @@
+// MI355X backend: device state of one work unit and batched template processing.
+//
+// Per batch of B templates one HIP graph replays
+//   H2D params -> H2D thresholds -> memset counters -> n_steps -> FFT pass 1
+//   (fused resampling) -> pass 2 -> pass 3 (untangle + power spectrum) ->
+//   harmonic sum + compaction -> D2H counters + first candidate slots
+// with a single host synchronisation per batch. The reference issues ~11
+// launches, 5 blocking transfers and up to ~6 MB of device->host copies per
+// template (cuda/app/demod_binary_cuda.cu:416-965, demod_binary_hs_cuda.cu:302-677).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+
+#include "../core/errors.hpp"
+#include "../core/gsl_compat.hpp"
+#include "../core/cpu_backend.hpp"
+#include "../core/log.hpp"
+#include "../core/rngmed.hpp"
+#include "../hip/fft_kernels.hpp"
+#include "../hip/hs_kernels.hpp"
+#include "../hip/resample_kernels.hpp"
+#include "../hip/whiten_kernels.hpp"
+#include "backend.hpp"
+#include "hip_engine.hpp"
+
+namespace brp {
+
+using hipk::TemplateDev;
+
+bool make_fft_plan(uint32_t M, FFTPlan3& plan) {
+  plan = FFTPlan3();
+  static const uint32_t p3[] = {256, 128, 64};
+  static const uint32_t p12[] = {512, 384, 256, 192, 128, 96, 64, 48, 32, 16};
+  for (uint32_t L3 : p3) {
+    if (M % L3) continue;
+    const uint32_t R = M / L3;
+    uint32_t best1 = 0, best2 = 0;
+    for (uint32_t L1 : p12) {
+      if (R % L1) continue;
+      const uint32_t L2 = R / L1;
+      if (!hipk::pass12_length_supported(L2)) continue;
+      if (L1 < L2) continue;
+      if (!best1 || (L1 - L2) < (best1 - best2)) {
+        best1 = L1;
+        best2 = L2;
+      }
+    }
+    if (best1) {
+      plan.M = M;
+      plan.L1 = best1;
+      plan.L2 = best2;
+      plan.L3 = L3;
+      plan.ncol1 = plan.ncol2 = 16;
+      plan.rows3 = 8;
+      return true;
+    }
+  }
+  return false;
+}
+
+namespace {
+
+template <typename T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  int alloc(size_t count) {
+    release();
+    if (count == 0) return 0;
+    if (hipMalloc(&p, count * sizeof(T)) != hipSuccess) {
+      p = nullptr;
+      return RADPUL_HIP_MEM_ALLOC_DEVICE;
+    }
+    n = count;
+    return 0;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+  ~DevBuf() { release(); }
+};
+
+template <typename T>
+struct PinnedBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  int alloc(size_t count) {
+    release();
+    if (count == 0) return 0;
+    if (hipHostMalloc(&p, count * sizeof(T), hipHostMallocDefault) != hipSuccess) {
+      p = nullptr;
+      return RADPUL_HIP_MEM_ALLOC_HOST;
+    }
+    n = count;
+    return 0;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    n = 0;
+  }
+  ~PinnedBuf() { release(); }
+};
+
+// W_{2N}^j = exp(-i pi j / N) as a two-level float table
+void build_twiddles(uint64_t period, std::vector<float2>& hi, std::vector<float2>& lo) {
+  const uint32_t nlo = 1u << hipk::kTwLoBits;
+  const uint64_t nhi = (period + nlo - 1) / nlo + 1;
+  hi.resize(nhi);
+  lo.resize(nlo);
+  const long double pi = 3.14159265358979323846264338327950288L;
+  auto w = [&](uint64_t j) {
+    j %= period;
+    const long double a = -2.0L * pi * static_cast<long double>(j) / static_cast<long double>(period);
+    return make_float2(static_cast<float>(cosl(a)), static_cast<float>(sinl(a)));
+  };
+  for (uint64_t i = 0; i < nhi; ++i) hi[i] = w(i * nlo);
+  for (uint32_t j = 0; j < nlo; ++j) lo[j] = w(j);
+}
+
+}  // namespace
+
+struct HipEngine::Impl {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  int batch = 4;
+  uint32_t cap = 1u << 16;      // candidate slots per (template, level)
+  uint32_t kcopy = 2048;        // slots copied back eagerly
+
+  SearchGeometry g;
+  FFTPlan3 plan;
+  bool ready = false;
+  float mu0 = 0.0f;
+  uint32_t ps_stride = 0;
+  uint32_t i_start = 0;
+
+  DevBuf<float> series;
+  DevBuf<float2> buf;           // [batch][M]
+  DevBuf<float> ps;             // [batch][ps_stride]
+  DevBuf<double> partials;      // [batch][wg1]
+  DevBuf<TemplateDev> tmpl;     // [batch]
+  DevBuf<float> thr;            // [5]
+  DevBuf<uint32_t> counts;      // [batch][5]
+  DevBuf<uint2> cands;          // [batch][5][cap]
+  DevBuf<float2> tw_hi, tw_lo;
+
+  PinnedBuf<TemplateDev> h_tmpl;
+  PinnedBuf<float> h_thr;
+  PinnedBuf<uint32_t> h_counts;
+  PinnedBuf<uint2> h_cands;     // [batch][5][kcopy]
+
+  std::map<int, hipGraphExec_t> graphs;
+  BackendStats st;
+
+  hipk::TwiddleTable twt() const {
+    hipk::TwiddleTable t;
+    t.hi = tw_hi.p;
+    t.lo = tw_lo.p;
+    t.period = 2ull * plan.M * 2ull;  // 2N = 4M
+    return t;
+  }
+
+  ~Impl() {
+    for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second);
+    if (ev0) (void)hipEventDestroy(ev0);
+    if (ev1) (void)hipEventDestroy(ev1);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+
+  // Enqueue the whole per-batch pipeline on `stream` (also used for capture).
+  hipError_t enqueue(int nb) {
+    hipError_t e;
+    e = hipMemcpyAsync(tmpl.p, h_tmpl.p, sizeof(TemplateDev) * nb, hipMemcpyHostToDevice, stream);
+    if (e != hipSuccess) return e;
+    e = hipMemcpyAsync(thr.p, h_thr.p, sizeof(float) * kNumHarmonicLevels, hipMemcpyHostToDevice, stream);
+    if (e != hipSuccess) return e;
+    e = hipMemsetAsync(counts.p, 0, sizeof(uint32_t) * kNumHarmonicLevels * nb, stream);
+    if (e != hipSuccess) return e;
+    e = hipk::launch_nsteps(tmpl.p, nb, stream);
+    if (e != hipSuccess) return e;
+    const hipk::TwiddleTable tw = twt();
+    hipk::Pass1Args a1{};
+    a1.out = buf.p;
+    a1.L2L3 = plan.L2 * plan.L3;
+    a1.L3 = plan.L3;
+    a1.tw = tw;
+    a1.series = series.p;
+    a1.n_unpadded = g.n_unpadded;
+    a1.tmpl = tmpl.p;
+    a1.partials = partials.p;
+    e = hipk::launch_pass1(plan, hipk::P1_RESAMPLE, a1, nb, stream);
+    if (e != hipSuccess) return e;
+    hipk::Pass2Args a2{};
+    a2.buf = buf.p;
+    a2.L1 = plan.L1;
+    a2.L2L3 = plan.L2 * plan.L3;
+    a2.L3 = plan.L3;
+    a2.tw = tw;
+    e = hipk::launch_pass2(plan, a2, nb, stream);
+    if (e != hipSuccess) return e;
+    hipk::Pass3Args a3{};
+    a3.buf = buf.p;
+    a3.L1 = plan.L1;
+    a3.L2 = plan.L2;
+    a3.L3 = plan.L3;
+    a3.C = plan.L1 * plan.L2;
+    a3.M = plan.M;
+    a3.tw = tw;
+    a3.limit = std::min(g.harmonic_idx_hi, g.fft_size);
+    a3.ps = ps.p;
+    a3.ps_stride = ps_stride;
+    a3.norm = static_cast<float>(1.0 / g.nsamples);
+    a3.tmpl = tmpl.p;
+    a3.partials = partials.p;
+    a3.n_partials = plan.wg1();
+    e = hipk::launch_pass3(plan, hipk::P3_POWER, a3, nb, stream);
+    if (e != hipSuccess) return e;
+    hipk::HSArgs ah{};
+    ah.ps = ps.p;
+    ah.ps_stride = ps_stride;
+    ah.w2 = g.window_2;
+    ah.fhi = g.fundamental_idx_hi;
+    ah.hhi = std::min(g.harmonic_idx_hi, g.fft_size);
+    ah.i_start = i_start;
+    ah.thr = thr.p;
+    ah.counts = counts.p;
+    ah.cands = cands.p;
+    ah.cap = cap;
+    e = hipk::launch_harmonic_sum(ah, nb, stream);
+    if (e != hipSuccess) return e;
+    e = hipMemcpyAsync(h_counts.p, counts.p, sizeof(uint32_t) * kNumHarmonicLevels * nb, hipMemcpyDeviceToHost,
+                       stream);
+    if (e != hipSuccess) return e;
+    e = hipMemcpy2DAsync(h_cands.p, sizeof(uint2) * kcopy, cands.p, sizeof(uint2) * cap, sizeof(uint2) * kcopy,
+                         static_cast<size_t>(kNumHarmonicLevels) * nb, hipMemcpyDeviceToHost, stream);
+    return e;
+  }
+};
+
+HipEngine::HipEngine() : impl_(new Impl) {}
+HipEngine::~HipEngine() {
+  if (impl_ && impl_->stream) (void)hipStreamSynchronize(impl_->stream);
+  delete impl_;
+}
+
+int HipEngine::init(int device, int batch) {
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+    log_message(LOG_ERROR, true, "No HIP device available.\n");
+    return RADPUL_HIP_DEVICE_FIND;
+  }
+  if (device < 0) {
+    const char* env = std::getenv("BRP_DEVICE");
+    device = env ? std::atoi(env) : 0;
+  }
+  if (device >= ndev) {
+    log_message(LOG_ERROR, true, "Requested device %d but only %d present.\n", device, ndev);
+    return RADPUL_HIP_DEVICE_SET;
+  }
+  BRP_HIP_CHECK(hipSetDevice(device), RADPUL_HIP_DEVICE_SET);
+  impl_->device = device;
+  impl_->batch = batch > 0 ? batch : 4;
+  BRP_HIP_CHECK(hipStreamCreateWithFlags(&impl_->stream, hipStreamNonBlocking), RADPUL_HIP_DEVICE_SET);
+  BRP_HIP_CHECK(hipEventCreate(&impl_->ev0), RADPUL_HIP_DEVICE_SET);
+  BRP_HIP_CHECK(hipEventCreate(&impl_->ev1), RADPUL_HIP_DEVICE_SET);
+  hipDeviceProp_t prop;
+  BRP_HIP_CHECK(hipGetDeviceProperties(&prop, device), RADPUL_HIP_DEVICE_PROP);
+  log_message(LOG_INFO, true, "Using HIP device #%d: %s (%s, %d CUs, %.1f GB)\n", device, prop.name,
+              prop.gcnArchName, prop.multiProcessorCount, prop.totalGlobalMem / 1e9);
+  return 0;
+}
+
+int HipEngine::setup(const SearchGeometry& g, const std::vector<float>& series, float mu0) {
+  Impl& d = *impl_;
+  BRP_HIP_CHECK(hipSetDevice(d.device), RADPUL_HIP_DEVICE_SET);
+  for (auto& kv : d.graphs) (void)hipGraphExecDestroy(kv.second);
+  d.graphs.clear();
+  d.g = g;
+  d.mu0 = mu0;
+  if (g.nsamples % 2 || !make_fft_plan(g.nsamples / 2, d.plan)) {
+    log_message(LOG_ERROR, true, "Unsupported FFT length %u (need N/2 = L1*L2*L3 from the compiled set).\n",
+                g.nsamples);
+    return RADPUL_HIP_FFT_PLAN;
+  }
+  log_message(LOG_DEBUG, true, "FFT plan: N=%u M=%u = %u x %u x %u\n", g.nsamples, d.plan.M, d.plan.L1, d.plan.L2,
+              d.plan.L3);
+  const uint32_t limit = std::min(g.harmonic_idx_hi, g.fft_size);
+  d.ps_stride = std::max<uint32_t>((std::max(limit, g.fundamental_idx_hi) + 63) / 64 * 64, 64);
+  d.i_start = (g.window_2 >= 8) ? ((g.window_2 - 8) / 16) * 16 + 8 : 8;
+  if (d.i_start > g.window_2) d.i_start = 8;  // unreachable; keeps the invariant i_start <= w2 for w2 >= 8
+  int rc;
+  const size_t B = static_cast<size_t>(d.batch);
+  if ((rc = d.series.alloc(g.n_unpadded))) return rc;
+  if ((rc = d.buf.alloc(B * d.plan.M))) return rc;
+  if ((rc = d.ps.alloc(B * d.ps_stride))) return rc;
+  if ((rc = d.partials.alloc(B * d.plan.wg1()))) return rc;
+  if ((rc = d.tmpl.alloc(B))) return rc;
+  if ((rc = d.thr.alloc(kNumHarmonicLevels))) return rc;
+  if ((rc = d.counts.alloc(B * kNumHarmonicLevels))) return rc;
+  if ((rc = d.cands.alloc(B * kNumHarmonicLevels * d.cap))) return rc;
+  if ((rc = d.h_tmpl.alloc(B))) return rc;
+  if ((rc = d.h_thr.alloc(kNumHarmonicLevels))) return rc;
+  if ((rc = d.h_counts.alloc(B * kNumHarmonicLevels))) return rc;
+  if ((rc = d.h_cands.alloc(B * kNumHarmonicLevels * d.kcopy))) return rc;
+  std::vector<float2> hi, lo;
+  build_twiddles(4ull * d.plan.M, hi, lo);
+  if ((rc = d.tw_hi.alloc(hi.size()))) return rc;
+  if ((rc = d.tw_lo.alloc(lo.size()))) return rc;
+  BRP_HIP_CHECK(hipMemcpy(d.tw_hi.p, hi.data(), hi.size() * sizeof(float2), hipMemcpyHostToDevice),
+                RADPUL_HIP_MEM_COPY_HOST_DEVICE);
+  BRP_HIP_CHECK(hipMemcpy(d.tw_lo.p, lo.data(), lo.size() * sizeof(float2), hipMemcpyHostToDevice),
+                RADPUL_HIP_MEM_COPY_HOST_DEVICE);
+  BRP_HIP_CHECK(hipMemcpy(d.series.p, series.data(), g.n_unpadded * sizeof(float), hipMemcpyHostToDevice),
+                RADPUL_HIP_MEM_COPY_HOST_DEVICE);
+  d.ready = true;
+  return 0;
+}
+
+int HipEngine::upload_series(const std::vector<float>& series, float mu0) {
+  Impl& d = *impl_;
+  d.mu0 = mu0;
+  BRP_HIP_CHECK(hipMemcpy(d.series.p, series.data(), d.g.n_unpadded * sizeof(float), hipMemcpyHostToDevice),
+                RADPUL_HIP_MEM_COPY_HOST_DEVICE);
+  return 0;
+}
+
+int HipEngine::whiten(const SearchOptions& opt, const std::vector<ZapRange>& zaps, std::vector<float>& series) {
+  Impl& d = *impl_;
+  const SearchGeometry& g = d.g;
+  auto t0 = std::chrono::steady_clock::now();
+  int32_t seed;
+  std::memcpy(&seed, series.data(), sizeof(seed));
+  log_message(LOG_INFO, true, "Seed for random number generator is %d.\n", seed);
+  const uint32_t fft_size = g.fft_size, M = d.plan.M;
+  if (fft_size < opt.window) return RADPUL_EVAL;
+  DevBuf<float2> spec, z;
+  DevBuf<float> psw, med;
+  int rc;
+  if ((rc = spec.alloc(fft_size))) return rc;
+  if ((rc = psw.alloc(fft_size))) return rc;
+  const uint32_t white_size = fft_size - opt.window + 1;
+  if ((rc = med.alloc(white_size))) return rc;
+  float2* work = d.buf.p;  // M complex scratch (batch slot 0)
+  const hipk::TwiddleTable tw = d.twt();
+  hipStream_t s = d.stream;
+  // forward r2c of the zero-padded series
+  hipk::Pass1Args a1{};
+  a1.out = work;
+  a1.L2L3 = d.plan.L2 * d.plan.L3;
+  a1.L3 = d.plan.L3;
+  a1.tw = tw;
+  a1.real_in = d.series.p;
+  a1.n_real = g.n_unpadded;
+  BRP_HIP_CHECK(hipk::launch_pass1(d.plan, hipk::P1_REAL, a1, 1, s), RADPUL_HIP_KERNEL_INVOKE);
+  hipk::Pass2Args a2{};
+  a2.buf = work;
+  a2.L1 = d.plan.L1;
+  a2.L2L3 = d.plan.L2 * d.plan.L3;
+  a2.L3 = d.plan.L3;
+  a2.tw = tw;
+  BRP_HIP_CHECK(hipk::launch_pass2(d.plan, a2, 1, s), RADPUL_HIP_KERNEL_INVOKE);
+  hipk::Pass3Args a3{};
+  a3.buf = work;
+  a3.L1 = d.plan.L1;
+  a3.L2 = d.plan.L2;
+  a3.L3 = d.plan.L3;
+  a3.C = d.plan.L1 * d.plan.L2;
+  a3.M = M;
+  a3.tw = tw;
+  a3.limit = fft_size;
+  a3.spec = spec.p;
+  BRP_HIP_CHECK(hipk::launch_pass3(d.plan, hipk::P3_COMPLEX, a3, 1, s), RADPUL_HIP_KERNEL_INVOKE);
+  BRP_HIP_CHECK(hipk::launch_whiten_power(spec.p, fft_size, psw.p, s), RADPUL_HIP_KERNEL_INVOKE);
+  if (hipk::running_median_supported(opt.window)) {
+    BRP_HIP_CHECK(hipk::launch_running_median(psw.p, fft_size, opt.window, med.p, s), RADPUL_HIP_KERNEL_INVOKE);
+  } else {
+    // very wide windows: exact host running median
+    std::vector<float> h_ps(fft_size), h_med(white_size);
+    BRP_HIP_CHECK(hipMemcpyAsync(h_ps.data(), psw.p, fft_size * sizeof(float), hipMemcpyDeviceToHost, s),
+                  RADPUL_HIP_MEM_COPY_DEVICE_HOST);
+    BRP_HIP_CHECK(hipStreamSynchronize(s), RADPUL_HIP_MEM_COPY_DEVICE_HOST);
+    running_median(h_ps.data(), fft_size, opt.window, h_med.data());
+    BRP_HIP_CHECK(hipMemcpyAsync(med.p, h_med.data(), white_size * sizeof(float), hipMemcpyHostToDevice, s),
+                  RADPUL_HIP_MEM_COPY_HOST_DEVICE);
+    BRP_HIP_CHECK(hipStreamSynchronize(s), RADPUL_HIP_MEM_COPY_HOST_DEVICE);
+  }
+  BRP_HIP_CHECK(hipk::launch_whiten_scale(spec.p, med.p, white_size, g.window_2, s), RADPUL_HIP_KERNEL_INVOKE);
+  // RFI zapping: noise drawn on the host in the reference order (GSL-compatible RNG)
+  ZapNoise noise;
+  make_zap_noise(seed, g, opt, zaps, noise);
+  DevBuf<uint32_t> zbins;
+  DevBuf<float2> znoise;
+  const uint32_t nz = static_cast<uint32_t>(noise.bin.size());
+  if (nz) {
+    std::vector<float2> zn(nz);
+    for (uint32_t i = 0; i < nz; ++i) zn[i] = make_float2(noise.re[i], noise.im[i]);
+    if ((rc = zbins.alloc(nz))) return rc;
+    if ((rc = znoise.alloc(nz))) return rc;
+    BRP_HIP_CHECK(hipMemcpyAsync(zbins.p, noise.bin.data(), nz * sizeof(uint32_t), hipMemcpyHostToDevice, s),
+                  RADPUL_HIP_MEM_COPY_HOST_DEVICE);
+    BRP_HIP_CHECK(hipMemcpyAsync(znoise.p, zn.data(), nz * sizeof(float2), hipMemcpyHostToDevice, s),
+                  RADPUL_HIP_MEM_COPY_HOST_DEVICE);
+    BRP_HIP_CHECK(hipk::launch_zap(spec.p, fft_size, zbins.p, znoise.p, nz, s), RADPUL_HIP_KERNEL_INVOKE);
+  }
+  // inverse c2r: tangle, conj-FFT, natural order, scale by 1/sqrt(N), keep n_unpadded
+  if ((rc = z.alloc(M))) return rc;
+  BRP_HIP_CHECK(hipk::launch_tangle(spec.p, M, fft_size, g.window_2, tw, z.p, s), RADPUL_HIP_KERNEL_INVOKE);
+  a1 = hipk::Pass1Args{};
+  a1.out = work;
+  a1.L2L3 = d.plan.L2 * d.plan.L3;
+  a1.L3 = d.plan.L3;
+  a1.tw = tw;
+  a1.cplx_in = z.p;
+  BRP_HIP_CHECK(hipk::launch_pass1(d.plan, hipk::P1_COMPLEX_CONJ, a1, 1, s), RADPUL_HIP_KERNEL_INVOKE);
+  BRP_HIP_CHECK(hipk::launch_pass2(d.plan, a2, 1, s), RADPUL_HIP_KERNEL_INVOKE);
+  hipk::Pass3PlainArgs ap{};
+  ap.buf = work;
+  ap.L1 = d.plan.L1;
+  ap.L2 = d.plan.L2;
+  ap.L3 = d.plan.L3;
+  ap.C = d.plan.L1 * d.plan.L2;
+  ap.tw = tw;
+  ap.scale = static_cast<float>(1.0 / std::sqrt(static_cast<float>(g.nsamples)));
+  ap.real_out = d.series.p;
+  ap.n_out = g.n_unpadded;
+  BRP_HIP_CHECK(hipk::launch_pass3_plain(d.plan, ap, s), RADPUL_HIP_KERNEL_INVOKE);
+  BRP_HIP_CHECK(hipMemcpyAsync(series.data(), d.series.p, g.n_unpadded * sizeof(float), hipMemcpyDeviceToHost, s),
+                RADPUL_HIP_MEM_COPY_DEVICE_HOST);
+  BRP_HIP_CHECK(hipStreamSynchronize(s), RADPUL_HIP_KERNEL_INVOKE);
+  d.mu0 = 0.0f;  // whitened series has its DC (and first window_2 bins) removed
+  d.st.whiten_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return 0;
+}
+
+int HipEngine::process(const TemplateInput* t, int n, const float thr[kNumHarmonicLevels],
+                       std::vector<TemplateCands>& out) {
+  Impl& d = *impl_;
+  if (!d.ready) return RADPUL_EMISC;
+  BRP_HIP_CHECK(hipSetDevice(d.device), RADPUL_HIP_DEVICE_SET);  // worker threads drive their own device
+  out.clear();
+  out.resize(n);
+  const SearchGeometry& g = d.g;
+  for (int off = 0; off < n; off += d.batch) {
+    const int nb = std::min(d.batch, n - off);
+    for (int k = 0; k < nb; ++k) {
+      TemplateDev td{};
+      td.p = make_resamp_params(g.nsamples, g.n_unpadded, g.fft_size, g.dt, g.step_inv, t[off + k].P,
+                                t[off + k].tau, t[off + k].Psi0);
+      td.n_steps = 0;
+      td.mu0 = d.mu0;
+      d.h_tmpl.p[k] = td;
+    }
+    std::memcpy(d.h_thr.p, thr, sizeof(float) * kNumHarmonicLevels);
+    hipGraphExec_t exec = nullptr;
+    auto it = d.graphs.find(nb);
+    const bool use_graph = std::getenv("BRP_NO_GRAPH") == nullptr;
+    if (use_graph) {
+      if (it == d.graphs.end()) {
+        hipGraph_t graph;
+        BRP_HIP_CHECK(hipStreamBeginCapture(d.stream, hipStreamCaptureModeThreadLocal), RADPUL_HIP_GRAPH);
+        hipError_t e = d.enqueue(nb);
+        hipError_t e2 = hipStreamEndCapture(d.stream, &graph);
+        if (e != hipSuccess || e2 != hipSuccess) {
+          log_message(LOG_ERROR, true, "Graph capture failed: %s / %s\n", hipGetErrorName(e), hipGetErrorName(e2));
+          return RADPUL_HIP_GRAPH;
+        }
+        BRP_HIP_CHECK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0), RADPUL_HIP_GRAPH);
+        (void)hipGraphDestroy(graph);
+        d.graphs[nb] = exec;
+      } else {
+        exec = it->second;
+      }
+    }
+    BRP_HIP_CHECK(hipEventRecord(d.ev0, d.stream), RADPUL_HIP_KERNEL_INVOKE);
+    if (use_graph) {
+      BRP_HIP_CHECK(hipGraphLaunch(exec, d.stream), RADPUL_HIP_GRAPH);
+    } else {
+      BRP_HIP_CHECK(d.enqueue(nb), RADPUL_HIP_KERNEL_INVOKE);
+    }
+    BRP_HIP_CHECK(hipEventRecord(d.ev1, d.stream), RADPUL_HIP_KERNEL_INVOKE);
+    BRP_HIP_CHECK(hipStreamSynchronize(d.stream), RADPUL_HIP_KERNEL_INVOKE);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, d.ev0, d.ev1);
+    d.st.gpu_ms += ms;
+    d.st.batches += 1;
+    d.st.templates += nb;
+    for (int k = 0; k < nb; ++k) {
+      TemplateCands& tc = out[off + k];
+      for (int h = 0; h < kNumHarmonicLevels; ++h) {
+        const uint32_t cnt = d.h_counts.p[k * kNumHarmonicLevels + h];
+        std::vector<BinPower>& lv = tc.level[h];
+        lv.clear();
+        if (cnt > d.cap) {
+          log_message(LOG_ERROR, true, "Candidate overflow (%u > %u) on level %d.\n", cnt, d.cap, h);
+          return RADPUL_HIP_CAND_OVERFLOW;
+        }
+        const uint2* src = d.h_cands.p + (static_cast<size_t>(k) * kNumHarmonicLevels + h) * d.kcopy;
+        std::vector<uint2> extra;
+        if (cnt > d.kcopy) {
+          extra.resize(cnt);
+          const uint2* dsrc = d.cands.p + (static_cast<size_t>(k) * kNumHarmonicLevels + h) * d.cap;
+          BRP_HIP_CHECK(hipMemcpy(extra.data(), dsrc, cnt * sizeof(uint2), hipMemcpyDeviceToHost),
+                        RADPUL_HIP_MEM_COPY_DEVICE_HOST);
+          src = extra.data();
+          d.st.overflow_reruns += 1;
+        }
+        lv.resize(cnt);
+        for (uint32_t q = 0; q < cnt; ++q) {
+          float p;
+          std::memcpy(&p, &src[q].y, sizeof(float));
+          lv[q] = BinPower{src[q].x, p};
+        }
+        std::sort(lv.begin(), lv.end(), [](const BinPower& a, const BinPower& b) { return a.bin < b.bin; });
+      }
+    }
+  }
+  return 0;
+}
+
+int HipEngine::power_spectrum(const TemplateInput& t, std::vector<float>& ps_out, uint32_t* n_steps) {
+  Impl& d = *impl_;
+  const SearchGeometry& g = d.g;
+  TemplateDev td{};
+  td.p = make_resamp_params(g.nsamples, g.n_unpadded, g.fft_size, g.dt, g.step_inv, t.P, t.tau, t.Psi0);
+  td.mu0 = d.mu0;
+  d.h_tmpl.p[0] = td;
+  hipStream_t s = d.stream;
+  BRP_HIP_CHECK(hipMemcpyAsync(d.tmpl.p, d.h_tmpl.p, sizeof(TemplateDev), hipMemcpyHostToDevice, s),
+                RADPUL_HIP_MEM_COPY_HOST_DEVICE);
+  BRP_HIP_CHECK(hipk::launch_nsteps(d.tmpl.p, 1, s), RADPUL_HIP_KERNEL_INVOKE);
+  const hipk::TwiddleTable tw = d.twt();
+  hipk::Pass1Args a1{};
+  a1.out = d.buf.p;
+  a1.L2L3 = d.plan.L2 * d.plan.L3;
+  a1.L3 = d.plan.L3;
+  a1.tw = tw;
+  a1.series = d.series.p;
+  a1.n_unpadded = g.n_unpadded;
+  a1.tmpl = d.tmpl.p;
+  a1.partials = d.partials.p;
+  BRP_HIP_CHECK(hipk::launch_pass1(d.plan, hipk::P1_RESAMPLE, a1, 1, s), RADPUL_HIP_KERNEL_INVOKE);
+  hipk::Pass2Args a2{};
+  a2.buf = d.buf.p;
+  a2.L1 = d.plan.L1;
+  a2.L2L3 = d.plan.L2 * d.plan.L3;
+  a2.L3 = d.plan.L3;
+  a2.tw = tw;
+  BRP_HIP_CHECK(hipk::launch_pass2(d.plan, a2, 1, s), RADPUL_HIP_KERNEL_INVOKE);
+  DevBuf<float> full;
+  int rc;
+  if ((rc = full.alloc(g.fft_size))) return rc;
+  hipk::Pass3Args a3{};
+  a3.buf = d.buf.p;
+  a3.L1 = d.plan.L1;
+  a3.L2 = d.plan.L2;
+  a3.L3 = d.plan.L3;
+  a3.C = d.plan.L1 * d.plan.L2;
+  a3.M = d.plan.M;
+  a3.tw = tw;
+  a3.limit = g.fft_size;
+  a3.ps = full.p;
+  a3.ps_stride = g.fft_size;
+  a3.norm = static_cast<float>(1.0 / g.nsamples);
+  a3.tmpl = d.tmpl.p;
+  a3.partials = d.partials.p;
+  a3.n_partials = d.plan.wg1();
+  BRP_HIP_CHECK(hipk::launch_pass3(d.plan, hipk::P3_POWER, a3, 1, s), RADPUL_HIP_KERNEL_INVOKE);
+  ps_out.resize(g.fft_size);
+  BRP_HIP_CHECK(hipMemcpyAsync(ps_out.data(), full.p, g.fft_size * sizeof(float), hipMemcpyDeviceToHost, s),
+                RADPUL_HIP_MEM_COPY_DEVICE_HOST);
+  BRP_HIP_CHECK(hipMemcpyAsync(d.h_tmpl.p, d.tmpl.p, sizeof(TemplateDev), hipMemcpyDeviceToHost, s),
+                RADPUL_HIP_MEM_COPY_DEVICE_HOST);
+  BRP_HIP_CHECK(hipStreamSynchronize(s), RADPUL_HIP_KERNEL_INVOKE);
+  if (n_steps) *n_steps = d.h_tmpl.p[0].n_steps;
+  return 0;
+}
+
+BackendStats HipEngine::stats() const { return impl_->st; }
+int HipEngine::device() const { return impl_->device; }
+const FFTPlan3& HipEngine::plan() const { return impl_->plan; }
+int HipEngine::batch() const { return impl_->batch; }
+
+// ------------------------------------------------------------------ Backend
+namespace {
+class HipBackend final : public Backend {
+ public:
+  const char* name() const override { return "hip"; }
+  int init(int device, int batch) { return eng_.init(device, batch); }
+  int setup(const SearchGeometry& g, const SearchOptions& opt, std::vector<float>& series,
+            const std::vector<ZapRange>& zaps) override {
+    double mean = 0.0;
+    for (float v : series) mean += v;
+    mean = series.empty() ? 0.0 : mean / series.size();
+    int rc = eng_.setup(g, series, static_cast<float>(mean));
+    if (rc) return rc;
+    if (opt.white) return eng_.whiten(opt, zaps, series);
+    return 0;
+  }
+  int process(const TemplateInput* t, int n, const float thr[kNumHarmonicLevels],
+              std::vector<TemplateCands>& out) override {
+    return eng_.process(t, n, thr, out);
+  }
+  int preferred_batch() const override { return eng_.batch(); }
+  BackendStats stats() const override { return eng_.stats(); }
+
+ private:
+  HipEngine eng_;
+};
+}  // namespace
+
+std::unique_ptr<Backend> make_hip_backend(int device, int batch, int* err) {
+  auto b = std::make_unique<HipBackend>();
+  int rc = b->init(device, batch);
+  if (err) *err = rc;
+  if (rc) return nullptr;
+  return b;
+}
+
+}  // namespace brp

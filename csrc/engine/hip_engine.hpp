@@ -1,0 +1,41 @@
+// Low-level MI355X engine (used by the HIP backend, the Python bindings and tests).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <vector>
+
+#include "../hip/fft_plan.hpp"
+#include "backend.hpp"
+
+namespace brp {
+
+class HipEngine {
+ public:
+  HipEngine();
+  ~HipEngine();
+  HipEngine(const HipEngine&) = delete;
+  HipEngine& operator=(const HipEngine&) = delete;
+
+  int init(int device, int batch);
+  // allocate per-WU buffers, upload the series; mu0 = reference level
+  // subtracted before the FFT (keeps the padding correction well conditioned)
+  int setup(const SearchGeometry& g, const std::vector<float>& series, float mu0);
+  int upload_series(const std::vector<float>& series, float mu0);
+  // whitening + zapping on the device; `series` receives the whitened data
+  int whiten(const SearchOptions& opt, const std::vector<ZapRange>& zaps, std::vector<float>& series);
+  int process(const TemplateInput* t, int n, const float thr[kNumHarmonicLevels], std::vector<TemplateCands>& out);
+  // test hooks
+  int power_spectrum(const TemplateInput& t, std::vector<float>& ps, uint32_t* n_steps);
+
+  BackendStats stats() const;
+  int device() const;
+  int batch() const;
+  const FFTPlan3& plan() const;
+
+ private:
+  struct Impl;
+  Impl* impl_;
+};
+
+}  // namespace brp

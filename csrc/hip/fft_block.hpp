@@ -1,0 +1,260 @@
+// Workgroup-level FFT building blocks for gfx950.
+//
+// A workgroup transforms NCOL independent sequences of length L that live in
+// LDS. Each stage is a Stockham radix-R step (natural-order output, no bit
+// reversal): butterfly j reads elements j + q*L/R, applies the stage twiddle
+// W_{Ns*R}^{(j mod Ns) q}, does an R-point DFT in registers and writes element
+// (j/Ns)*Ns*R + (j mod Ns) + q*Ns. Stage twiddles come from a per-length LDS
+// table W_L^e (filled once per workgroup), so no transcendental is evaluated in
+// the inner loop.
+//
+// Two LDS layouts:
+//   column layout (ROWMAJOR=false): element (r, c) at r*NCOL + c, lanes walk c
+//     fastest -> the strided "column" passes read/write 8*NCOL contiguous bytes
+//     per row of the global array (128 B for NCOL=16).
+//   row layout    (ROWMAJOR=true):  element (r, c) at c*(L+1) + r, lanes walk r
+//     fastest -> the contiguous "row" pass streams whole rows.
+#pragma once
+
+#include "hip_common.hpp"
+
+namespace brp {
+namespace hipk {
+
+// ---------------------------------------------------------------- radix DFTs
+// Forward DFTs (kernel exp(-2 pi i / R)), in place on registers.
+template <int R>
+struct Dft;
+
+template <>
+struct Dft<2> {
+  static __device__ __forceinline__ void run(float2* v) {
+    const float2 a = v[0], b = v[1];
+    v[0] = cadd(a, b);
+    v[1] = csub(a, b);
+  }
+};
+
+template <>
+struct Dft<3> {
+  static __device__ __forceinline__ void run(float2* v) {
+    const float s = 0.86602540378443864676f;  // sin(2pi/3)
+    const float2 t1 = cadd(v[1], v[2]);
+    const float2 t2 = make_float2(v[0].x - 0.5f * t1.x, v[0].y - 0.5f * t1.y);
+    const float2 t3 = mul_mi(cscale(csub(v[1], v[2]), s));
+    v[0] = cadd(v[0], t1);
+    v[1] = cadd(t2, t3);
+    v[2] = csub(t2, t3);
+  }
+};
+
+template <>
+struct Dft<4> {
+  static __device__ __forceinline__ void run(float2* v) {
+    const float2 a0 = cadd(v[0], v[2]), a1 = csub(v[0], v[2]);
+    const float2 b0 = cadd(v[1], v[3]), b1 = mul_mi(csub(v[1], v[3]));
+    v[0] = cadd(a0, b0);
+    v[1] = cadd(a1, b1);
+    v[2] = csub(a0, b0);
+    v[3] = csub(a1, b1);
+  }
+};
+
+template <>
+struct Dft<5> {
+  static __device__ __forceinline__ void run(float2* v) {
+    const float c1 = 0.30901699437494742410f, c2 = -0.80901699437494742410f;
+    const float s1 = 0.95105651629515357212f, s2 = 0.58778525229247312917f;
+    const float2 a1 = cadd(v[1], v[4]), a2 = cadd(v[2], v[3]);
+    const float2 b1 = csub(v[1], v[4]), b2 = csub(v[2], v[3]);
+    const float2 x0 = v[0];
+    const float2 p1 = make_float2(x0.x + c1 * a1.x + c2 * a2.x, x0.y + c1 * a1.y + c2 * a2.y);
+    const float2 p2 = make_float2(x0.x + c2 * a1.x + c1 * a2.x, x0.y + c2 * a1.y + c1 * a2.y);
+    const float2 q1 = mul_mi(make_float2(s1 * b1.x + s2 * b2.x, s1 * b1.y + s2 * b2.y));
+    const float2 q2 = mul_mi(make_float2(s2 * b1.x - s1 * b2.x, s2 * b1.y - s1 * b2.y));
+    v[0] = make_float2(x0.x + a1.x + a2.x, x0.y + a1.y + a2.y);
+    v[1] = cadd(p1, q1);
+    v[4] = csub(p1, q1);
+    v[2] = cadd(p2, q2);
+    v[3] = csub(p2, q2);
+  }
+};
+
+template <>
+struct Dft<8> {
+  static __device__ __forceinline__ void run(float2* v) {
+    const float r = 0.70710678118654752440f;
+    float2 e[4] = {v[0], v[2], v[4], v[6]};
+    float2 o[4] = {v[1], v[3], v[5], v[7]};
+    Dft<4>::run(e);
+    Dft<4>::run(o);
+    // o[k] *= W8^k
+    o[1] = make_float2(r * (o[1].x + o[1].y), r * (o[1].y - o[1].x));
+    o[2] = mul_mi(o[2]);
+    o[3] = make_float2(r * (o[3].y - o[3].x), -r * (o[3].x + o[3].y));
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      v[k] = cadd(e[k], o[k]);
+      v[k + 4] = csub(e[k], o[k]);
+    }
+  }
+};
+
+template <>
+struct Dft<16> {
+  static __device__ __forceinline__ void run(float2* v) {
+    // x[a + 4b]: DFT4 over b for each a, twiddle W16^{a k1}, DFT4 over a
+    float2 u[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      float2 t[4] = {v[a], v[a + 4], v[a + 8], v[a + 12]};
+      Dft<4>::run(t);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) u[a][k] = t[k];
+    }
+    const float c1 = 0.92387953251128675613f, s1 = 0.38268343236508977173f;
+    const float r = 0.70710678118654752440f;
+    // W16^1, W16^2, W16^3, W16^4 = -i, W16^6, W16^9
+    const float2 w1 = make_float2(c1, -s1), w2 = make_float2(r, -r), w3 = make_float2(s1, -c1);
+    const float2 w6 = make_float2(-r, -r), w9 = make_float2(-c1, s1);
+    u[1][1] = cmul(u[1][1], w1);
+    u[1][2] = cmul(u[1][2], w2);
+    u[1][3] = cmul(u[1][3], w3);
+    u[2][1] = cmul(u[2][1], w2);
+    u[2][2] = mul_mi(u[2][2]);
+    u[2][3] = cmul(u[2][3], w6);
+    u[3][1] = cmul(u[3][1], w3);
+    u[3][2] = cmul(u[3][2], w6);
+    u[3][3] = cmul(u[3][3], w9);
+#pragma unroll
+    for (int k1 = 0; k1 < 4; ++k1) {
+      float2 t[4] = {u[0][k1], u[1][k1], u[2][k1], u[3][k1]};
+      Dft<4>::run(t);
+#pragma unroll
+      for (int k2 = 0; k2 < 4; ++k2) v[k1 + 4 * k2] = t[k2];
+    }
+  }
+};
+
+// ------------------------------------------------------------ block FFT core
+template <int L, int NCOL, int TPC, bool ROWMAJOR>
+struct BlockLayout {
+  static constexpr int kThreads = NCOL * TPC;
+  static constexpr int kLds = ROWMAJOR ? NCOL * (L + 1) : L * NCOL;  // float2 elements
+  __device__ __forceinline__ static int idx(int r, int c) { return ROWMAJOR ? c * (L + 1) + r : r * NCOL + c; }
+  __device__ __forceinline__ static void coords(int tid, int& c, int& tj) {
+    if (ROWMAJOR) {
+      tj = tid % TPC;
+      c = tid / TPC;
+    } else {
+      c = tid % NCOL;
+      tj = tid / NCOL;
+    }
+  }
+};
+
+// One Stockham stage LDS -> LDS (in place, two barriers).
+template <int L, int NCOL, int TPC, bool ROWMAJOR, int R, int Ns>
+__device__ __forceinline__ void block_stage(float2* lds, const float2* tw_lds) {
+  using Lay = BlockLayout<L, NCOL, TPC, ROWMAJOR>;
+  constexpr int kBf = L / R;                       // butterflies per column
+  constexpr int kNb = (kBf + TPC - 1) / TPC;       // butterflies per thread
+  int c, tj;
+  Lay::coords(threadIdx.x, c, tj);
+  float2 v[kNb][R];
+#pragma unroll
+  for (int u = 0; u < kNb; ++u) {
+    const int j = tj + u * TPC;
+    if (kBf % TPC == 0 || j < kBf) {
+#pragma unroll
+      for (int q = 0; q < R; ++q) v[u][q] = lds[Lay::idx(j + q * kBf, c)];
+      if (Ns > 1) {
+        const int jm = j % Ns;
+#pragma unroll
+        for (int q = 1; q < R; ++q) v[u][q] = cmul(v[u][q], tw_lds[(jm * q * (L / (Ns * R))) % L]);
+      }
+      Dft<R>::run(v[u]);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < kNb; ++u) {
+    const int j = tj + u * TPC;
+    if (kBf % TPC == 0 || j < kBf) {
+      const int base = (j / Ns) * Ns * R + (j % Ns);
+#pragma unroll
+      for (int q = 0; q < R; ++q) lds[Lay::idx(base + q * Ns, c)] = v[u][q];
+    }
+  }
+  __syncthreads();
+}
+
+template <int L, int NCOL, int TPC, bool ROWMAJOR, int Ns, int... Rs>
+struct BlockStages;
+
+template <int L, int NCOL, int TPC, bool ROWMAJOR, int Ns>
+struct BlockStages<L, NCOL, TPC, ROWMAJOR, Ns> {
+  static __device__ __forceinline__ void run(float2*, const float2*) {}
+};
+
+template <int L, int NCOL, int TPC, bool ROWMAJOR, int Ns, int R, int... Rest>
+struct BlockStages<L, NCOL, TPC, ROWMAJOR, Ns, R, Rest...> {
+  static __device__ __forceinline__ void run(float2* lds, const float2* tw) {
+    block_stage<L, NCOL, TPC, ROWMAJOR, R, Ns>(lds, tw);
+    BlockStages<L, NCOL, TPC, ROWMAJOR, Ns * R, Rest...>::run(lds, tw);
+  }
+};
+
+template <int... Rs>
+struct Product;
+template <>
+struct Product<> {
+  static constexpr int value = 1;
+};
+template <int R, int... Rest>
+struct Product<R, Rest...> {
+  static constexpr int value = R * Product<Rest...>::value;
+};
+
+// Radix decomposition for each supported sub-FFT length.
+template <int L>
+struct Radices;
+template <> struct Radices<16> { template <template <int...> class F> using apply = F<16>; };
+template <> struct Radices<32> { template <template <int...> class F> using apply = F<2, 16>; };
+template <> struct Radices<48> { template <template <int...> class F> using apply = F<3, 16>; };
+template <> struct Radices<64> { template <template <int...> class F> using apply = F<4, 16>; };
+template <> struct Radices<80> { template <template <int...> class F> using apply = F<5, 16>; };
+template <> struct Radices<96> { template <template <int...> class F> using apply = F<3, 2, 16>; };
+template <> struct Radices<128> { template <template <int...> class F> using apply = F<8, 16>; };
+template <> struct Radices<160> { template <template <int...> class F> using apply = F<5, 2, 16>; };
+template <> struct Radices<192> { template <template <int...> class F> using apply = F<3, 4, 16>; };
+template <> struct Radices<240> { template <template <int...> class F> using apply = F<3, 5, 16>; };
+template <> struct Radices<256> { template <template <int...> class F> using apply = F<16, 16>; };
+template <> struct Radices<320> { template <template <int...> class F> using apply = F<5, 4, 16>; };
+template <> struct Radices<384> { template <template <int...> class F> using apply = F<3, 8, 16>; };
+template <> struct Radices<512> { template <template <int...> class F> using apply = F<2, 16, 16>; };
+
+template <int L, int NCOL, int TPC, bool ROWMAJOR>
+struct BlockFFT {
+  template <int... Rs>
+  struct Impl {
+    static_assert(Product<Rs...>::value == L, "radix list must multiply to L");
+    static __device__ __forceinline__ void run(float2* lds, const float2* tw) {
+      BlockStages<L, NCOL, TPC, ROWMAJOR, 1, Rs...>::run(lds, tw);
+    }
+  };
+  static __device__ __forceinline__ void run(float2* lds, const float2* tw) {
+    Radices<L>::template apply<Impl>::run(lds, tw);
+  }
+};
+
+// Fill a per-length twiddle table W_L^e (e < L) in LDS from the global table
+// W_{2N} (2N multiple of L).
+template <int L>
+__device__ __forceinline__ void load_stage_twiddles(float2* tw_lds, const TwiddleTable& t) {
+  const uint32_t step = static_cast<uint32_t>(t.period / L);
+  for (int e = threadIdx.x; e < L; e += blockDim.x) tw_lds[e] = tw_lookup32(t, static_cast<uint32_t>(e) * step);
+}
+
+}  // namespace hipk
+}  // namespace brp

@@ -1,0 +1,95 @@
+// Kernel argument blocks and launchers of the three FFT passes
+// (implementation: fft_passes.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "../core/resamp_math.hpp"
+#include "fft_plan.hpp"
+#include "hip_common.hpp"
+
+namespace brp {
+namespace hipk {
+
+// Per-template device parameters (one entry per template of a batch).
+struct TemplateDev {
+  ResampParams p;
+  uint32_t n_steps;   // samples taken from the series (rest is mean padding)
+  float mu0;          // reference level subtracted before the FFT
+  uint32_t pad[2];
+};
+
+enum Pass1Mode : int {
+  P1_RESAMPLE = 0,   // fused nearest-neighbour resampling of the time series
+  P1_REAL = 1,       // zero-padded real series
+  P1_COMPLEX_CONJ = 2,  // complex input, conjugated (inverse transform)
+};
+
+struct Pass1Args {
+  float2* out;                 // [batch][M]
+  uint32_t L2L3, L3;
+  TwiddleTable tw;
+  // P1_RESAMPLE
+  const float* series;         // n_unpadded samples (shared by the batch)
+  uint32_t n_unpadded;
+  const TemplateDev* tmpl;     // [batch]
+  double* partials;            // [batch][wg1] sums of (sample - mu0)
+  // P1_REAL
+  const float* real_in;
+  uint32_t n_real;
+  // P1_COMPLEX_CONJ
+  const float2* cplx_in;
+};
+
+struct Pass2Args {
+  float2* buf;                 // [batch][M], in place
+  uint32_t L1, L2L3, L3;
+  TwiddleTable tw;
+};
+
+enum Pass3Mode : int {
+  P3_POWER = 0,     // untangle + power spectrum (+ mean-padding correction)
+  P3_COMPLEX = 1,   // untangle, complex half spectrum out (whitening)
+};
+
+struct Pass3Args {
+  const float2* buf;           // [batch][M]
+  uint32_t L1, L2, L3, C;      // C = L1*L2 rows
+  uint32_t M;
+  TwiddleTable tw;
+  uint32_t limit;              // write bins k < limit only
+  // P3_POWER
+  float* ps;                   // [batch][ps_stride]
+  uint32_t ps_stride;
+  float norm;                  // 1/N (float)
+  const TemplateDev* tmpl;     // n_steps per template
+  const double* partials;      // [batch][n_partials]
+  uint32_t n_partials;
+  // P3_COMPLEX
+  float2* spec;                // fft_size complex bins
+};
+
+// plain row pass of the inverse transform: conj, scale, write the first
+// n_out real samples of the natural-order output
+struct Pass3PlainArgs {
+  const float2* buf;
+  uint32_t L1, L2, L3, C;
+  TwiddleTable tw;
+  float scale;
+  float* real_out;
+  uint32_t n_out;              // real samples to write
+};
+
+hipError_t launch_pass1(const FFTPlan3& plan, Pass1Mode mode, const Pass1Args& a, int batch, hipStream_t s);
+hipError_t launch_pass2(const FFTPlan3& plan, const Pass2Args& a, int batch, hipStream_t s);
+hipError_t launch_pass3(const FFTPlan3& plan, Pass3Mode mode, const Pass3Args& a, int batch, hipStream_t s);
+hipError_t launch_pass3_plain(const FFTPlan3& plan, const Pass3PlainArgs& a, hipStream_t s);
+
+// lengths with compiled kernels
+bool pass12_length_supported(uint32_t L);
+bool pass3_length_supported(uint32_t L);
+
+}  // namespace hipk
+}  // namespace brp

@@ -1,0 +1,379 @@
+// Three-pass packed real FFT for gfx950 with fused prologue/epilogue:
+//   pass 1: nearest-neighbour resampling gather (or real / complex load) fused
+//           into the load of L1-point column FFTs
+//   pass 2: L2-point column FFTs, in place
+//   pass 3: L3-point row FFTs + real-FFT untangle + normalised power spectrum
+//           (+ analytic mean-padding correction), natural-order output
+// See fft_plan.hpp for the index algebra. Replaces the reference's cuFFT /
+// clFFT / FFTW calls (cuda/app/demod_binary_cuda.cu:849-965,
+// opencl/app/demod_binary_ocl.cpp:972-1314, demod_binary_fft_fftw.c:46-113) and
+// its resampling kernels (cuda/app/demod_binary_cuda.cuh:69-184).
+#include "fft_block.hpp"
+#include "fft_kernels.hpp"
+
+namespace brp {
+namespace hipk {
+
+namespace {
+
+constexpr int kNcol = 16;
+
+template <int L>
+constexpr int tpc_for() {
+  return (L / 16) < 1 ? 1 : (L / 16);
+}
+
+// block-wide deterministic sum of one double per thread (result valid in all threads)
+template <int NT>
+__device__ __forceinline__ double block_sum(double v, double* scratch) {
+  v = wave_sum(v);
+  const int w = threadIdx.x / kWave;
+  constexpr int kWaves = (NT + kWave - 1) / kWave;
+  __syncthreads();
+  if ((threadIdx.x % kWave) == 0) scratch[w] = v;
+  __syncthreads();
+  double t = 0.0;
+#pragma unroll
+  for (int i = 0; i < kWaves; ++i) t += scratch[i];
+  __syncthreads();
+  return t;
+}
+
+__device__ __forceinline__ float resample_sample(uint32_t m, const TemplateDev& td, const float* series,
+                                                 uint32_t n_unpadded) {
+  if (m >= td.n_steps) return 0.0f;
+  const float dt = resamp_del_t(m, td.p, kSinLut, kCosLut);
+  int idx = resamp_nearest(m, dt);
+  idx = idx < 0 ? 0 : (idx >= static_cast<int>(n_unpadded) ? static_cast<int>(n_unpadded) - 1 : idx);
+  return series[idx] - td.mu0;
+}
+
+// ------------------------------------------------------------------ pass 1
+template <int L, int MODE>
+__global__ void __launch_bounds__(kNcol * tpc_for<L>()) pass1_kernel(Pass1Args a) {
+  constexpr int TPC = tpc_for<L>();
+  constexpr int NT = kNcol * TPC;
+  using Lay = BlockLayout<L, kNcol, TPC, false>;
+  __shared__ __attribute__((aligned(16))) float2 smem[Lay::kLds + L + 16];
+  float2* data = smem;
+  float2* twl = smem + Lay::kLds;
+  double* red = reinterpret_cast<double*>(smem + Lay::kLds + L);
+
+  const int b = blockIdx.y;
+  const uint32_t nblk3 = a.L3 / kNcol;
+  const uint32_t n2 = blockIdx.x / nblk3;
+  const uint32_t col_base = n2 * a.L3 + (blockIdx.x % nblk3) * kNcol;
+  const size_t M = static_cast<size_t>(L) * a.L2L3;
+
+  load_stage_twiddles<L>(twl, a.tw);
+  int c, tj;
+  Lay::coords(threadIdx.x, c, tj);
+
+  double sum = 0.0;
+  if (MODE == P1_RESAMPLE) {
+    const TemplateDev td = a.tmpl[b];
+#pragma unroll 4
+    for (int r = tj; r < L; r += TPC) {
+      const uint32_t n = r * a.L2L3 + col_base + c;
+      const float x0 = resample_sample(2 * n, td, a.series, a.n_unpadded);
+      const float x1 = resample_sample(2 * n + 1, td, a.series, a.n_unpadded);
+      sum += static_cast<double>(x0) + static_cast<double>(x1);
+      data[Lay::idx(r, c)] = make_float2(x0, x1);
+    }
+  } else if (MODE == P1_REAL) {
+    for (int r = tj; r < L; r += TPC) {
+      const uint32_t n = r * a.L2L3 + col_base + c;
+      const float x0 = (2 * n < a.n_real) ? a.real_in[2 * n] : 0.0f;
+      const float x1 = (2 * n + 1 < a.n_real) ? a.real_in[2 * n + 1] : 0.0f;
+      data[Lay::idx(r, c)] = make_float2(x0, x1);
+    }
+  } else {
+    for (int r = tj; r < L; r += TPC) {
+      const uint32_t n = r * a.L2L3 + col_base + c;
+      data[Lay::idx(r, c)] = conjf2(a.cplx_in[static_cast<size_t>(b) * M + n]);
+    }
+  }
+  __syncthreads();
+  BlockFFT<L, kNcol, TPC, false>::run(data, twl);
+
+  float2* out = a.out + static_cast<size_t>(b) * M;
+  const uint32_t tw_step = n2 * 4u * a.L3;  // W_{L1 L2}^{n2 k1} = W_2N^{n2 k1 4 L3}
+  for (int k1 = tj; k1 < L; k1 += TPC) {
+    float2 v = data[Lay::idx(k1, c)];
+    v = cmul(v, tw_lookup32(a.tw, tw_step * static_cast<uint32_t>(k1)));
+    out[static_cast<size_t>(k1) * a.L2L3 + col_base + c] = v;
+  }
+  if (MODE == P1_RESAMPLE) {
+    const double tot = block_sum<NT>(sum, red);
+    if (threadIdx.x == 0) a.partials[static_cast<size_t>(b) * gridDim.x + blockIdx.x] = tot;
+  }
+}
+
+// ------------------------------------------------------------------ pass 2
+template <int L>
+__global__ void __launch_bounds__(kNcol * tpc_for<L>()) pass2_kernel(Pass2Args a) {
+  constexpr int TPC = tpc_for<L>();
+  using Lay = BlockLayout<L, kNcol, TPC, false>;
+  __shared__ __attribute__((aligned(16))) float2 smem[Lay::kLds + L];
+  float2* data = smem;
+  float2* twl = smem + Lay::kLds;
+
+  const int b = blockIdx.y;
+  const uint32_t nblk3 = a.L3 / kNcol;
+  const uint32_t k1 = blockIdx.x / nblk3;
+  const uint32_t n3_0 = (blockIdx.x % nblk3) * kNcol;
+  const size_t M = static_cast<size_t>(a.L1) * a.L2L3;
+  float2* buf = a.buf + static_cast<size_t>(b) * M;
+  const size_t base = static_cast<size_t>(k1) * a.L2L3 + n3_0;
+
+  load_stage_twiddles<L>(twl, a.tw);
+  int c, tj;
+  Lay::coords(threadIdx.x, c, tj);
+  for (int r = tj; r < L; r += TPC) data[Lay::idx(r, c)] = buf[base + static_cast<size_t>(r) * a.L3 + c];
+  __syncthreads();
+  BlockFFT<L, kNcol, TPC, false>::run(data, twl);
+  const uint32_t n3 = n3_0 + c;
+  for (int k2 = tj; k2 < L; k2 += TPC) {
+    float2 v = data[Lay::idx(k2, c)];
+    // W_M^{n3 (k1 + L1 k2)} = W_2N^{4 n3 (k1 + L1 k2)}
+    v = cmul(v, tw_lookup32(a.tw, 4u * n3 * (k1 + a.L1 * static_cast<uint32_t>(k2))));
+    buf[base + static_cast<size_t>(k2) * a.L3 + c] = v;
+  }
+}
+
+// ------------------------------------------------------------------ pass 3
+__device__ __forceinline__ size_t row_base(uint32_t c, uint32_t L1, uint32_t L2, uint32_t L3) {
+  const uint32_t k1 = c % L1, k2 = c / L1;
+  return (static_cast<size_t>(k1) * L2 + k2) * L3;
+}
+
+// X_k of the real FFT from Z_k and Z_{M-k} of the packed complex FFT.
+__device__ __forceinline__ float2 untangle(float2 zk, float2 zmk, const TwiddleTable& tw, uint32_t k) {
+  const float2 bc = conjf2(zmk);
+  const float2 e = cscale(cadd(zk, bc), 0.5f);
+  const float2 o = cscale(csub(zk, bc), 0.5f);
+  const float2 w = tw_lookup32(tw, 2u * k);  // W_N^k
+  return cadd(e, mul_mi(cmul(w, o)));
+}
+
+// FFT of the padding indicator 1[m >= n_s] (m < N) at bin k in [1, N/2]:
+// S_k = -(sin(pi n_s k / N) / sin(pi k / N)) * exp(-i pi (n_s - 1) k / N)
+__device__ __forceinline__ float2 padding_spectrum(const TwiddleTable& tw, uint32_t n_s, uint32_t k) {
+  const float2 ta = tw_lookup(tw, static_cast<uint64_t>(n_s) * k);
+  const float2 tk = tw_lookup32(tw, k);
+  const float2 tc = tw_lookup(tw, static_cast<uint64_t>(n_s - 1) * k);
+  const float ratio = ta.y / tk.y;
+  return make_float2(-ratio * tc.x, -ratio * tc.y);
+}
+
+template <int L, int ROWS, int MODE>
+__global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Args a) {
+  constexpr int TPC = tpc_for<L>();
+  constexpr int NSLOT = 2 * ROWS;
+  constexpr int NT = NSLOT * TPC;
+  using Lay = BlockLayout<L, NSLOT, TPC, true>;
+  __shared__ __attribute__((aligned(16))) float2 smem[Lay::kLds + L + 16];
+  float2* data = smem;
+  float2* twl = smem + Lay::kLds;
+  double* red = reinterpret_cast<double*>(smem + Lay::kLds + L);
+
+  const int b = blockIdx.y;
+  const float2* buf = a.buf + static_cast<size_t>(b) * a.M;
+  const uint32_t c0 = blockIdx.x * ROWS;
+
+  load_stage_twiddles<L>(twl, a.tw);
+  {
+    int slot, tj;
+    Lay::coords(threadIdx.x, slot, tj);
+    const uint32_t cs = c0 + (slot % ROWS);
+    const uint32_t row = (slot < ROWS) ? cs : (a.C - cs) % a.C;
+    const float2* src = buf + row_base(row < a.C ? row : 0, a.L1, a.L2, a.L3);
+    for (int r = tj; r < L; r += TPC) data[Lay::idx(r, slot)] = src[r];
+  }
+  // mean-padding correction delta = (sum of (sample - mu0)) / n_steps
+  double delta = 0.0;
+  uint32_t n_s = 0;
+  if (MODE == P3_POWER) {
+    double part = 0.0;
+    const double* pp = a.partials + static_cast<size_t>(b) * a.n_partials;
+    for (uint32_t i = threadIdx.x; i < a.n_partials; i += NT) part += pp[i];
+    const double tot = block_sum<NT>(part, red);
+    n_s = a.tmpl[b].n_steps;
+    delta = tot / static_cast<double>(n_s);
+  }
+  __syncthreads();
+  BlockFFT<L, NSLOT, TPC, true>::run(data, twl);
+
+  const float2 dS = make_float2(static_cast<float>(delta), 0.0f);
+  auto emit = [&](uint32_t k, float2 x) {
+    if (k >= a.limit) return;
+    if (MODE == P3_POWER) {
+      float p = 0.0f;
+      if (k != 0) {
+        if (n_s > 0) {
+          const float2 s = padding_spectrum(a.tw, n_s, k);
+          x = make_float2(x.x + dS.x * s.x, x.y + dS.x * s.y);
+        }
+        const double re = x.x, im = x.y;
+        p = static_cast<float>(static_cast<double>(a.norm) * (re * re + im * im));
+      }
+      a.ps[static_cast<size_t>(b) * a.ps_stride + k] = p;
+    } else {
+      a.spec[k] = x;
+    }
+  };
+
+  // untangle: thread -> (slot s, k3 stream), rows c <= C/2 own their bins
+  const int s = threadIdx.x % ROWS;
+  const int t = threadIdx.x / ROWS;
+  constexpr int kStreams = NT / ROWS;
+  const uint32_t c = c0 + s;
+  const uint32_t half = a.C / 2;
+  if (c <= half) {
+    for (int k3 = t; k3 < L; k3 += kStreams) {
+      const float2 zk = data[Lay::idx(k3, s)];
+      float2 zm;
+      if (c == 0) {
+        zm = data[Lay::idx((L - k3) % L, s)];
+      } else {
+        zm = data[Lay::idx(L - 1 - k3, ROWS + s)];
+      }
+      const uint32_t k = c + a.C * static_cast<uint32_t>(k3);
+      emit(k, untangle(zk, zm, a.tw, k));
+      if (c != 0 && c != half) {
+        const uint32_t kk = a.M - k;
+        emit(kk, untangle(zm, zk, a.tw, kk));
+      }
+      if (c == 0 && k3 == 0) {
+        // Nyquist bin M: X_M = Re Z_0 - Im Z_0
+        emit(a.M, make_float2(zk.x - zk.y, 0.0f));
+      }
+    }
+  }
+}
+
+template <int L, int ROWS>
+__global__ void __launch_bounds__(ROWS * tpc_for<L>()) pass3_plain_kernel(Pass3PlainArgs a) {
+  constexpr int TPC = tpc_for<L>();
+  constexpr int NT = ROWS * TPC;
+  using Lay = BlockLayout<L, ROWS, TPC, true>;
+  __shared__ __attribute__((aligned(16))) float2 smem[Lay::kLds + L];
+  float2* data = smem;
+  float2* twl = smem + Lay::kLds;
+  const uint32_t c0 = blockIdx.x * ROWS;
+  load_stage_twiddles<L>(twl, a.tw);
+  {
+    int slot, tj;
+    Lay::coords(threadIdx.x, slot, tj);
+    const float2* src = a.buf + row_base(c0 + slot, a.L1, a.L2, a.L3);
+    for (int r = tj; r < L; r += TPC) data[Lay::idx(r, slot)] = src[r];
+  }
+  __syncthreads();
+  BlockFFT<L, ROWS, TPC, true>::run(data, twl);
+  // natural-order output z[c + C*k3] = conj(Z)*scale -> real samples 2n, 2n+1
+  const int s = threadIdx.x % ROWS;
+  const int t = threadIdx.x / ROWS;
+  constexpr int kStreams = NT / ROWS;
+  const uint32_t c = c0 + s;
+  for (int k3 = t; k3 < L; k3 += kStreams) {
+    const float2 z = data[Lay::idx(k3, s)];
+    const size_t n = c + static_cast<size_t>(a.C) * k3;
+    if (2 * n < a.n_out) a.real_out[2 * n] = z.x * a.scale;
+    if (2 * n + 1 < a.n_out) a.real_out[2 * n + 1] = -z.y * a.scale;
+  }
+}
+
+}  // namespace
+
+// ------------------------------------------------------------ dispatch glue
+#define BRP_P12_LENGTHS(X) X(16) X(32) X(48) X(64) X(96) X(128) X(192) X(256) X(384) X(512)
+#define BRP_P3_LENGTHS(X) X(64) X(128) X(256)
+
+bool pass12_length_supported(uint32_t L) {
+  switch (L) {
+#define X(n) case n:
+    BRP_P12_LENGTHS(X)
+#undef X
+    return true;
+    default: return false;
+  }
+}
+
+bool pass3_length_supported(uint32_t L) {
+  switch (L) {
+#define X(n) case n:
+    BRP_P3_LENGTHS(X)
+#undef X
+    return true;
+    default: return false;
+  }
+}
+
+hipError_t launch_pass1(const FFTPlan3& plan, Pass1Mode mode, const Pass1Args& a, int batch, hipStream_t s) {
+  const dim3 grid(plan.wg1(), batch);
+  switch (plan.L1) {
+#define X(n)                                                                                          \
+  case n: {                                                                                           \
+    const dim3 block(kNcol * tpc_for<n>());                                                           \
+    if (mode == P1_RESAMPLE) hipLaunchKernelGGL((pass1_kernel<n, P1_RESAMPLE>), grid, block, 0, s, a); \
+    else if (mode == P1_REAL) hipLaunchKernelGGL((pass1_kernel<n, P1_REAL>), grid, block, 0, s, a);    \
+    else hipLaunchKernelGGL((pass1_kernel<n, P1_COMPLEX_CONJ>), grid, block, 0, s, a);                 \
+    break;                                                                                            \
+  }
+    BRP_P12_LENGTHS(X)
+#undef X
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_pass2(const FFTPlan3& plan, const Pass2Args& a, int batch, hipStream_t s) {
+  const dim3 grid(plan.wg2(), batch);
+  switch (plan.L2) {
+#define X(n)                                                                \
+  case n:                                                                   \
+    hipLaunchKernelGGL((pass2_kernel<n>), grid, dim3(kNcol * tpc_for<n>()), 0, s, a); \
+    break;
+    BRP_P12_LENGTHS(X)
+#undef X
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+constexpr int kRows3 = 8;
+
+hipError_t launch_pass3(const FFTPlan3& plan, Pass3Mode mode, const Pass3Args& a, int batch, hipStream_t s) {
+  if (plan.rows3 != kRows3) return hipErrorInvalidValue;
+  const dim3 grid(plan.wg3(), batch);
+  switch (plan.L3) {
+#define X(n)                                                                                              \
+  case n: {                                                                                               \
+    const dim3 block(2 * kRows3 * tpc_for<n>());                                                          \
+    if (mode == P3_POWER) hipLaunchKernelGGL((pass3_kernel<n, kRows3, P3_POWER>), grid, block, 0, s, a);  \
+    else hipLaunchKernelGGL((pass3_kernel<n, kRows3, P3_COMPLEX>), grid, block, 0, s, a);                 \
+    break;                                                                                                \
+  }
+    BRP_P3_LENGTHS(X)
+#undef X
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_pass3_plain(const FFTPlan3& plan, const Pass3PlainArgs& a, hipStream_t s) {
+  const dim3 grid(plan.wg3_plain());
+  switch (plan.L3) {
+#define X(n)                                                                                       \
+  case n:                                                                                          \
+    hipLaunchKernelGGL((pass3_plain_kernel<n, kRows3>), grid, dim3(kRows3 * tpc_for<n>()), 0, s, a); \
+    break;
+    BRP_P3_LENGTHS(X)
+#undef X
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace hipk
+}  // namespace brp

@@ -1,0 +1,70 @@
+// Shared device-side helpers for the MI355X (gfx950) kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+
+#include "../core/errors.hpp"
+#include "../core/log.hpp"
+
+namespace brp {
+namespace hipk {
+
+#define BRP_HIP_CHECK(expr, code)                                                                  \
+  do {                                                                                             \
+    hipError_t _e = (expr);                                                                        \
+    if (_e != hipSuccess) {                                                                        \
+      ::brp::log_message(::brp::LOG_ERROR, true, "HIP error %s at %s:%d: %s\n", hipGetErrorName(_e), \
+                         __FILE__, __LINE__, #expr);                                               \
+      return (code);                                                                               \
+    }                                                                                              \
+  } while (0)
+
+constexpr int kWave = 64;
+
+// Two-level table for W_{2N}^j = exp(-i pi j / N), j in [0, 2N):
+//   W^j = hi[j >> kTwLoBits] * lo[j & (2^kTwLoBits - 1)]
+// Both tables are tiny (L1/L2 resident); the product is accurate to ~1e-7.
+constexpr int kTwLoBits = 12;
+struct TwiddleTable {
+  const float2* hi;
+  const float2* lo;
+  uint64_t period;  // 2N
+};
+
+#if defined(__HIP__)
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+  return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ float2 conjf2(float2 a) { return make_float2(a.x, -a.y); }
+// multiply by -i (forward-transform rotation)
+__device__ __forceinline__ float2 mul_mi(float2 a) { return make_float2(a.y, -a.x); }
+__device__ __forceinline__ float2 cscale(float2 a, float s) { return make_float2(a.x * s, a.y * s); }
+
+__device__ __forceinline__ float2 tw_lookup(const TwiddleTable& t, uint64_t j) {
+  j %= t.period;
+  const float2 a = t.hi[j >> kTwLoBits];
+  const float2 b = t.lo[j & ((1u << kTwLoBits) - 1)];
+  return cmul(a, b);
+}
+// same for an exponent already known to be < period (32-bit fast path)
+__device__ __forceinline__ float2 tw_lookup32(const TwiddleTable& t, uint32_t j) {
+  const float2 a = t.hi[j >> kTwLoBits];
+  const float2 b = t.lo[j & ((1u << kTwLoBits) - 1)];
+  return cmul(a, b);
+}
+
+// wave-level sum (64 lanes) of a double
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+#endif  // __HIP__
+
+}  // namespace hipk
+}  // namespace brp

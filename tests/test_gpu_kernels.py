@@ -1,0 +1,108 @@
+"""HIP kernels vs the CPU golden model (run on an MI355X: pytest -m gpu)."""
+import numpy as np
+import pytest
+
+from boinc_app_eah_brp_amd.utils import synth
+
+from conftest import BANK, WU, ZAP
+
+pytestmark = pytest.mark.gpu
+
+OPT_BENCH = dict(f0=400.0, padding=3.0, fA=0.08, window=1000)
+
+
+def _engine(brp, geom, series, mu0=None, batch=2):
+    eng = brp.HipEngine()
+    eng.init(0, batch)
+    eng.setup(geom, np.ascontiguousarray(series, dtype=np.float32),
+              float(np.mean(series)) if mu0 is None else mu0)
+    return eng
+
+
+def _cpu_ps(brp, series, geom, P, tau, psi):
+    x, n_steps, mean = brp.cpu_resample(series, geom, P, tau, psi)
+    return brp.cpu_power_spectrum(x, geom["fft_size"]), n_steps
+
+
+@pytest.mark.parametrize("padding", [1.0, 3.0])
+def test_power_spectrum_small(brp, gpu, tmp_path, padding):
+    case = synth.synthetic_case(tmp_path, n=1 << 16, n_templates=4,
+                                inj=synth.Injection(f0=300.0, P_orb=800.0, tau=0.05, psi0=1.0, amplitude=2.0))
+    hdr, series, _ = brp.read_work_unit(case["wu"])
+    geom = brp.derive_geometry(hdr, dict(OPT_BENCH, padding=padding, f0=200.0, window=100))
+    eng = _engine(brp, geom, series)
+    for k in range(4):
+        P, tau, psi = (np.float32(case[key][k]) for key in ("P", "tau", "psi"))
+        ps_gpu, ns_gpu = eng.power_spectrum(float(P), float(tau), float(psi))
+        ps_cpu, ns_cpu = _cpu_ps(brp, series, geom, float(P), float(tau), float(psi))
+        assert ns_gpu == ns_cpu
+        scale = float(np.mean(ps_cpu[1:]))
+        err = np.abs(ps_gpu.astype(np.float64) - ps_cpu) / np.maximum(ps_cpu, scale)
+        assert err[1:].max() < 2e-4, (k, err.max(), int(np.argmax(err)))
+
+
+def test_power_spectrum_bench_size(brp, gpu):
+    """Benchmark geometry (2^22 samples, P=3 -> 3*2^22-point FFT) on the whitened reference WU."""
+    hdr, series, _ = brp.read_work_unit(str(WU))
+    opt = dict(OPT_BENCH, white=True)
+    geom = brp.derive_geometry(hdr, opt)
+    eng = _engine(brp, geom, series)
+    series = eng.whiten(opt, brp.read_zaplist(str(ZAP)), series)
+    P, tau, psi = brp.read_template_bank(str(BANK))
+    for k in (0, 1):
+        ps_gpu, ns_gpu = eng.power_spectrum(float(P[k]), float(tau[k]), float(psi[k]))
+        ps_cpu, ns_cpu = _cpu_ps(brp, series, geom, float(P[k]), float(tau[k]), float(psi[k]))
+        assert ns_gpu == ns_cpu
+        lim = geom["harmonic_idx_hi"]
+        scale = float(np.median(ps_cpu[geom["window_2"]:lim]))
+        err = np.abs(ps_gpu[1:lim].astype(np.float64) - ps_cpu[1:lim]) / np.maximum(ps_cpu[1:lim], scale)
+        assert np.percentile(err, 99.9) < 2e-5, (k, np.percentile(err, 99.9))
+        assert err.max() < 1e-3, (k, err.max(), int(np.argmax(err)) + 1)
+
+
+def test_harmonic_sum_matches_cpu_bitwise(brp, gpu, tmp_path):
+    """Same power spectrum in -> identical candidate bins and powers out."""
+    case = synth.synthetic_case(tmp_path, n=1 << 17, n_templates=2,
+                                inj=synth.Injection(f0=150.0, P_orb=900.0, tau=0.02, psi0=2.0, amplitude=3.0))
+    hdr, series, _ = brp.read_work_unit(case["wu"])
+    geom = brp.derive_geometry(hdr, dict(f0=120.0, padding=3.0, fA=0.08, window=100))
+    eng = _engine(brp, geom, series, batch=1)
+    P, tau, psi = (np.float32(case[key][0]) for key in ("P", "tau", "psi"))
+    thr = [4.0, 6.0, 9.0, 14.0, 24.0]  # low thresholds -> many candidates
+    out = eng.process(np.array([P]), np.array([tau]), np.array([psi]), thr)[0]
+    ps_gpu, _ = eng.power_spectrum(float(P), float(tau), float(psi))
+    ref, _ = brp.cpu_harmonic_sum(ps_gpu, geom, thr)
+    for h in range(5):
+        bins_g, pw_g = out[h]
+        bins_c, pw_c = ref[h]
+        assert len(bins_c) > 0
+        np.testing.assert_array_equal(bins_g, bins_c)
+        np.testing.assert_array_equal(pw_g, pw_c)
+
+
+def test_whitening_matches_cpu(brp, gpu, tmp_path):
+    case = synth.synthetic_case(tmp_path, n=1 << 16, n_templates=1)
+    hdr, series, _ = brp.read_work_unit(case["wu"])
+    opt = dict(f0=200.0, padding=3.0, fA=0.08, window=200, white=True)
+    geom = brp.derive_geometry(hdr, opt)
+    zaps = brp.read_zaplist(case["zap"])
+    w_cpu = brp.cpu_whiten(series, geom, opt, zaps)
+    eng = _engine(brp, geom, series)
+    w_gpu = eng.whiten(opt, zaps, series)
+    rms = float(np.sqrt(np.mean(w_cpu.astype(np.float64) ** 2)))
+    assert rms > 0
+    assert np.max(np.abs(w_gpu - w_cpu)) / rms < 1e-4
+
+
+def test_running_median_gpu_exact(brp, gpu, tmp_path):
+    """The device running median must be bit-identical to the host one (via whitening scale)."""
+    case = synth.synthetic_case(tmp_path, n=1 << 15, n_templates=1)
+    hdr, series, _ = brp.read_work_unit(case["wu"])
+    for window in (99, 100, 1000):
+        opt = dict(f0=200.0, padding=1.0, fA=0.08, window=window, white=True)
+        geom = brp.derive_geometry(hdr, opt)
+        w_cpu = brp.cpu_whiten(series, geom, opt, [])
+        eng = _engine(brp, geom, series)
+        w_gpu = eng.whiten(opt, [], series)
+        rms = float(np.sqrt(np.mean(w_cpu.astype(np.float64) ** 2)))
+        assert np.max(np.abs(w_gpu - w_cpu)) / rms < 1e-4, window
