@@ -129,18 +129,226 @@ int finalize_output(const SearchOptions& opt, const SearchGeometry& g, uint32_t 
   return write_results(opt.outputfile, cands, g.t_obs_d, info);
 }
 
+
+struct SearchSession::Impl {
+  SearchOptions opt;
+  SearchControl ctl;
+  TemplateBank bank;
+  WorkUnit wu;
+  SearchGeometry g;
+  SearchInfo info;
+  std::vector<ZapRange> zaps;
+  std::vector<TemplateInput> tin;
+  std::vector<std::unique_ptr<Backend>> backends;
+  std::vector<float> series;  // whitened (or raw) series used for templates
+};
+
+SearchSession::SearchSession() : impl_(new Impl) {}
+SearchSession::~SearchSession() = default;
+const SearchGeometry& SearchSession::geometry() const { return impl_->g; }
+const TemplateBank& SearchSession::bank() const { return impl_->bank; }
+const WorkUnit& SearchSession::work_unit() const { return impl_->wu; }
+const SearchOptions& SearchSession::options() const { return impl_->opt; }
+uint32_t SearchSession::total() const { return static_cast<uint32_t>(impl_->bank.size()); }
+
+BackendStats SearchSession::stats() const {
+  BackendStats t;
+  for (auto& be : impl_->backends) {
+    const BackendStats s = be->stats();
+    t.gpu_ms += s.gpu_ms;
+    t.whiten_ms += s.whiten_ms;
+    t.templates += s.templates;
+    t.batches += s.batches;
+    t.overflow_reruns += s.overflow_reruns;
+  }
+  return t;
+}
+
+int SearchSession::open(const SearchOptions& opt, const SearchControl& ctl) {
+  Impl& d = *impl_;
+  d.opt = opt;
+  d.ctl = ctl;
+  int rc = read_template_bank(opt.templatebank, d.bank);
+  if (rc) return rc;
+  log_message(LOG_DEBUG, true, "Total amount of templates: %zu\n", d.bank.size());
+  d.tin.resize(d.bank.size());
+  for (size_t t = 0; t < d.bank.size(); ++t)
+    d.tin[t] = TemplateInput{static_cast<float>(d.bank.P[t]), static_cast<float>(d.bank.tau[t]),
+                             static_cast<float>(d.bank.Psi0[t])};
+  rc = read_work_unit(opt.inputfile, d.wu);
+  if (rc) return rc;
+  if (opt.debug) log_header(d.wu.header);
+  sky_position(d.wu.header, d.info);
+  rc = derive_geometry(d.wu.header, opt, d.g);
+  if (rc) return rc;
+  if (opt.white) {
+    if (opt.zaplistfile.empty()) {
+      log_message(LOG_ERROR, true, "Whitening requested but no zaplist file given (-l).\n");
+      return RADPUL_EFILE;
+    }
+    rc = read_zaplist(opt.zaplistfile, d.zaps);
+    if (rc) return rc;
+  }
+  if (opt.debug) {
+    log_message(LOG_INFO, true, "Derived global search parameters:\n");
+    log_message(LOG_INFO, false, "f_A probability = %g\n", opt.fA);
+    log_message(LOG_INFO, false, "single bin prob(P_noise > P_thr) = %g\n", d.g.prob);
+    const char* names[5] = {"thr1", "thr2", "thr4", "thr8", "thr16"};
+    for (int h = 0; h < 5; ++h)
+      log_message(LOG_INFO, false, "%s = %g\n", names[h], 0.5 * chisq_Qinv_even(d.g.prob, 1 << h));
+  }
+  const int ngpu = opt.use_cpu ? 1 : std::max(1, ctl.gpus);
+  boinc::begin_critical_section();
+  for (int k = 0; k < ngpu; ++k) {
+    std::unique_ptr<Backend> b;
+    if (opt.use_cpu) {
+      b = make_cpu_backend();
+    } else {
+      int dev = opt.device;
+      if (!ctl.devices.empty()) dev = ctl.devices[k % ctl.devices.size()];
+      else if (ngpu > 1) dev = k;
+      else if (dev < 0 && boinc::init_data().gpu_device_num >= 0) dev = boinc::init_data().gpu_device_num;
+      int err = 0;
+      b = make_hip_backend(dev, opt.batch, &err);
+      if (!b) return err ? err : RADPUL_HIP_DEVICE_FIND;
+    }
+    d.backends.push_back(std::move(b));
+  }
+  boinc::end_critical_section();
+  return 0;
+}
+
+int SearchSession::prepare() {
+  Impl& d = *impl_;
+  d.series = d.wu.samples;
+  boinc::begin_critical_section();
+  int rc = d.backends[0]->setup(d.g, d.opt, d.series, d.zaps);
+  if (rc) return rc;
+  SearchOptions opt_nw = d.opt;
+  opt_nw.white = false;
+  for (size_t k = 1; k < d.backends.size(); ++k) {
+    std::vector<float> s = d.series;
+    rc = d.backends[k]->setup(d.g, opt_nw, s, d.zaps);
+    if (rc) return rc;
+  }
+  boinc::end_critical_section();
+  return 0;
+}
+
+int SearchSession::run(uint32_t begin, uint32_t end, CandidateTable& table, SearchResult& res,
+                       const TemplateHook& hook) {
+  Impl& d = *impl_;
+  const SearchGeometry& g = d.g;
+  end = std::min<uint32_t>(end, total());
+  if (begin >= end) return 0;
+  const int B = std::max(1, d.backends[0]->preferred_batch());
+
+  // Batches are dealt to the devices; results are applied in template order so
+  // the table evolves exactly as in the sequential reference loop
+  // (demod_binary.c:1180-1443). Device thresholds lag by at most the batches in
+  // flight, which only adds bins that the in-order application rejects.
+  std::mutex mu;
+  std::condition_variable cv;
+  std::map<uint32_t, BatchResult> ready;
+  float thr_shared[kNumHarmonicLevels];
+  table.thresholds(g.chi2_thr, thr_shared);
+  std::atomic<uint32_t> next_first{begin};
+  std::atomic<bool> stop{false};
+  auto worker = [&](Backend* be) {
+    for (;;) {
+      if (stop.load()) return;
+      const uint32_t first = next_first.fetch_add(static_cast<uint32_t>(B));
+      if (first >= end) return;
+      const int n = static_cast<int>(std::min<uint32_t>(B, end - first));
+      float thr[kNumHarmonicLevels];
+      {
+        std::lock_guard<std::mutex> lk(mu);
+        std::memcpy(thr, thr_shared, sizeof(thr));
+      }
+      BatchResult br;
+      br.first = first;
+      br.rc = be->process(&d.tin[first], n, thr, br.cands);
+      {
+        std::lock_guard<std::mutex> lk(mu);
+        ready.emplace(first, std::move(br));
+      }
+      cv.notify_all();
+    }
+  };
+  std::vector<std::thread> threads;
+  for (auto& be : d.backends) threads.emplace_back(worker, be.get());
+
+  uint32_t applied = begin;
+  int rc = 0;
+  bool quit = false;
+  std::set<uint32_t> pages;
+  SearchInfo& info = d.info;
+  while (applied < end && !quit) {
+    BatchResult br;
+    {
+      std::unique_lock<std::mutex> lk(mu);
+      cv.wait(lk, [&] { return ready.count(applied) > 0; });
+      br = std::move(ready[applied]);
+      ready.erase(applied);
+    }
+    if (br.rc) {
+      rc = br.rc;
+      break;
+    }
+    for (size_t k = 0; k < br.cands.size() && !quit; ++k) {
+      const uint32_t t = br.first + static_cast<uint32_t>(k);
+      const TemplateInput& ti = d.tin[t];
+      float thrA[kNumHarmonicLevels];
+      table.thresholds(g.chi2_thr, thrA);
+      unsigned char binned[kBinsScreensaver] = {0};
+      for (int h = 0; h < kNumHarmonicLevels; ++h) {
+        const std::vector<BinPower>& lv = br.cands[k].level[h];
+        table.apply_level(h, lv.data(), lv.size(), thrA[h], ti.P, ti.tau, ti.Psi0);
+        if (lv.empty()) continue;
+        pages.clear();
+        for (const BinPower& bp : lv)
+          if (bp.power > thrA[h]) pages.insert(bp.bin >> kLogPsPageSize);
+        res.dirty_pages += pages.size();
+        if (h == 2) {
+          const float powerscale = 100.0f / 255.0f;
+          const float stepscale = static_cast<float>(kBinsScreensaver) / static_cast<float>(g.fundamental_idx_hi);
+          for (const BinPower& bp : lv) {
+            const int bin_ss = static_cast<int>(stepscale * bp.bin);
+            if (bin_ss >= 0 && bin_ss < kBinsScreensaver && bp.power > powerscale * binned[bin_ss])
+              binned[bin_ss] = static_cast<unsigned char>(std::min(bp.power / powerscale, 255.0f));
+          }
+        }
+      }
+      info.orbital_radius = ti.tau;
+      info.orbital_period = ti.P;
+      info.orbital_phase = ti.Psi0;
+      std::memcpy(info.power_spectrum, binned, sizeof(binned));
+      ++res.templates_run;
+      if (hook && !hook(t + 1, info)) quit = true;
+    }
+    applied = br.first + static_cast<uint32_t>(br.cands.size());
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      table.thresholds(g.chi2_thr, thr_shared);
+    }
+  }
+  stop.store(true);
+  for (auto& th : threads) th.join();
+  if (quit) res.interrupted = true;
+  return rc;
+}
+
 int run_search(const SearchOptions& opt, const SearchControl& ctl, SearchResult& res) {
   const double t_start = now_s();
   res = SearchResult();
   log_message(LOG_INFO, true, "Starting data processing...\n");
-
-  // template bank (counted up front like the reference, demod_binary.c:506-544)
-  TemplateBank bank;
-  int rc = read_template_bank(opt.templatebank, bank);
+  SearchSession session;
+  int rc = session.open(opt, ctl);
   if (rc) return rc;
-  const uint32_t total = static_cast<uint32_t>(bank.size());
+  const uint32_t total = session.total();
   res.templates_total = total;
-  log_message(LOG_DEBUG, true, "Total amount of templates: %u\n", total);
+  res.geom = session.geometry();
+  const SearchGeometry& g = res.geom;
 
   // checkpoint restore (demod_binary.c:546-652)
   CandidateTable& table = res.table;
@@ -173,7 +381,8 @@ int run_search(const SearchOptions& opt, const SearchControl& ctl, SearchResult&
       }
       cp.header.originalfile[kFnLength - 1] = 0;
       if (opt.inputfile != cp.header.originalfile) {
-        log_message(LOG_ERROR, true, "Input file on command line %s doesn't agree with input file %s from checkpoint header.\n",
+        log_message(LOG_ERROR, true,
+                    "Input file on command line %s doesn't agree with input file %s from checkpoint header.\n",
                     opt.inputfile.c_str(), cp.header.originalfile);
         return RADPUL_EFILE;
       }
@@ -189,198 +398,47 @@ int run_search(const SearchOptions& opt, const SearchControl& ctl, SearchResult&
       }
     }
   }
-
-  // work unit
-  WorkUnit wu;
-  rc = read_work_unit(opt.inputfile, wu);
-  if (rc) return rc;
-  if (opt.debug) log_header(wu.header);
-  SearchInfo info;
-  sky_position(wu.header, info);
-  SearchGeometry& g = res.geom;
-  rc = derive_geometry(wu.header, opt, g);
-  if (rc) return rc;
-  std::vector<ZapRange> zaps;
-  if (opt.white) {
-    if (opt.zaplistfile.empty()) {
-      log_message(LOG_ERROR, true, "Whitening requested but no zaplist file given (-l).\n");
-      return RADPUL_EFILE;
-    }
-    rc = read_zaplist(opt.zaplistfile, zaps);
-    if (rc) return rc;
-  }
-  if (opt.debug) {
-    log_message(LOG_INFO, true, "Derived global search parameters:\n");
-    log_message(LOG_INFO, false, "f_A probability = %g\n", opt.fA);
-    log_message(LOG_INFO, false, "single bin prob(P_noise > P_thr) = %g\n", g.prob);
-    const char* names[5] = {"thr1", "thr2", "thr4", "thr8", "thr16"};
-    for (int h = 0; h < 5; ++h)
-      log_message(LOG_INFO, false, "%s = %g\n", names[h], 0.5 * chisq_Qinv_even(g.prob, 1 << h));
-  }
-
-  // backends: one per device, driven from this process
   const uint32_t begin = std::max(counter, ctl.begin);
   const uint32_t end = (ctl.end == 0 || ctl.end > total) ? total : ctl.end;
-  std::vector<std::unique_ptr<Backend>> backends;
-  const int ngpu = opt.use_cpu ? 1 : std::max(1, ctl.gpus);
-  boinc::begin_critical_section();
-  for (int k = 0; k < ngpu; ++k) {
-    std::unique_ptr<Backend> b;
-    if (opt.use_cpu) {
-      b = make_cpu_backend();
-    } else {
-      int dev = opt.device;
-      if (!ctl.devices.empty()) dev = ctl.devices[k % ctl.devices.size()];
-      else if (ngpu > 1) dev = k;
-      else if (dev < 0 && boinc::init_data().gpu_device_num >= 0) dev = boinc::init_data().gpu_device_num;
-      int err = 0;
-      b = make_hip_backend(dev, opt.batch, &err);
-      if (!b) return err ? err : RADPUL_HIP_DEVICE_FIND;
-    }
-    backends.push_back(std::move(b));
-  }
-  std::vector<float> series = wu.samples;
   if (begin < end) {
-    rc = backends[0]->setup(g, opt, series, zaps);
+    rc = session.prepare();
     if (rc) return rc;
-    SearchOptions opt_nw = opt;
-    opt_nw.white = false;
-    for (size_t k = 1; k < backends.size(); ++k) {
-      rc = backends[k]->setup(g, opt_nw, series, zaps);
-      if (rc) return rc;
-    }
   }
-  boinc::end_critical_section();
   res.t_setup = now_s() - t_start;
 
-  // template loop: batches dispatched to the devices, results applied in
-  // template order so the candidate table evolves exactly as in the
-  // sequential reference loop (demod_binary.c:1180-1443)
   const double t_loop = now_s();
-  const int B = std::max(1, backends[0]->preferred_batch());
-  std::vector<TemplateInput> tin(total);
-  for (uint32_t t = 0; t < total; ++t)
-    tin[t] = TemplateInput{static_cast<float>(bank.P[t]), static_cast<float>(bank.tau[t]), static_cast<float>(bank.Psi0[t])};
-
-  std::mutex mu;
-  std::condition_variable cv;
-  std::map<uint32_t, BatchResult> ready;
-  float thr_shared[kNumHarmonicLevels];
-  table.thresholds(g.chi2_thr, thr_shared);
-  std::atomic<uint32_t> next_first{begin};
-  std::atomic<bool> stop{false};
-  auto worker = [&](Backend* be) {
-    for (;;) {
-      if (stop.load()) return;
-      const uint32_t first = next_first.fetch_add(static_cast<uint32_t>(B));
-      if (first >= end) return;
-      const int n = static_cast<int>(std::min<uint32_t>(B, end - first));
-      float thr[kNumHarmonicLevels];
-      {
-        std::lock_guard<std::mutex> lk(mu);
-        std::memcpy(thr, thr_shared, sizeof(thr));
-      }
-      BatchResult br;
-      br.first = first;
-      br.rc = be->process(&tin[first], n, thr, br.cands);
-      {
-        std::lock_guard<std::mutex> lk(mu);
-        ready.emplace(first, std::move(br));
-      }
-      cv.notify_all();
-    }
-  };
-  std::vector<std::thread> threads;
-  for (auto& be : backends) threads.emplace_back(worker, be.get());
-
-  uint32_t applied = begin;
-  rc = 0;
-  std::set<uint32_t> pages;
   const char* fault = std::getenv("BRP_FAULT");
   long kill_after = -1;
   if (fault && std::strncmp(fault, "kill_after_template:", 20) == 0) kill_after = std::atol(fault + 20);
-  bool quit = false;
-  while (applied < end && !quit) {
-    BatchResult br;
-    {
-      std::unique_lock<std::mutex> lk(mu);
-      cv.wait(lk, [&] { return ready.count(applied) > 0; });
-      br = std::move(ready[applied]);
-      ready.erase(applied);
+  int cp_rc = 0;
+  auto hook = [&](uint32_t done, const SearchInfo& info) -> bool {
+    counter = done;
+    if (ipc::update_due()) ipc::update_shmem(info);
+    boinc::fraction_done((counter + 1.0) / total);
+    if (ctl.on_template) ctl.on_template(counter, total);
+    if (ctl.use_checkpoint && !opt.checkpointfile.empty() && boinc::time_to_checkpoint()) {
+      Checkpoint cp;
+      std::memset(&cp.header, 0, sizeof(cp.header));
+      cp.header.n_template = counter;
+      std::snprintf(cp.header.originalfile, sizeof(cp.header.originalfile), "%s", opt.inputfile.c_str());
+      std::memcpy(cp.cands, table.data(), sizeof(cp.cands));
+      cp_rc = write_checkpoint(opt.checkpointfile, cp);
+      if (cp_rc) return false;
+      log_message(LOG_INFO, true, "Checkpoint committed!\n");
+      boinc::checkpoint_completed();
     }
-    if (br.rc) {
-      rc = br.rc;
-      break;
-    }
-    for (size_t k = 0; k < br.cands.size() && !quit; ++k) {
-      const uint32_t t = br.first + static_cast<uint32_t>(k);
-      const TemplateInput& ti = tin[t];
-      float thrA[kNumHarmonicLevels];
-      table.thresholds(g.chi2_thr, thrA);
-      unsigned char binned[kBinsScreensaver] = {0};
-      for (int h = 0; h < kNumHarmonicLevels; ++h) {
-        const std::vector<BinPower>& lv = br.cands[k].level[h];
-        table.apply_level(h, lv.data(), lv.size(), thrA[h], ti.P, ti.tau, ti.Psi0);
-        pages.clear();
-        for (const BinPower& bp : lv)
-          if (bp.power > thrA[h]) pages.insert(bp.bin >> kLogPsPageSize);
-        res.dirty_pages += pages.size();
-        if (h == 2) {
-          const float powerscale = 100.0f / 255.0f;
-          const float stepscale = static_cast<float>(kBinsScreensaver) / static_cast<float>(g.fundamental_idx_hi);
-          for (const BinPower& bp : lv) {
-            const int bin_ss = static_cast<int>(stepscale * bp.bin);
-            if (bin_ss >= 0 && bin_ss < kBinsScreensaver && bp.power > powerscale * binned[bin_ss])
-              binned[bin_ss] = static_cast<unsigned char>(std::min(bp.power / powerscale, 255.0f));
-          }
-        }
-      }
-      info.orbital_radius = ti.tau;
-      info.orbital_period = ti.P;
-      info.orbital_phase = ti.Psi0;
-      std::memcpy(info.power_spectrum, binned, sizeof(binned));
-      if (ipc::update_due()) ipc::update_shmem(info);
-      ++counter;
-      ++res.templates_run;
-      boinc::fraction_done((counter + 1.0) / total);
-      if (ctl.on_template) ctl.on_template(counter, total);
-      if (ctl.use_checkpoint && !opt.checkpointfile.empty() && boinc::time_to_checkpoint()) {
-        Checkpoint cp;
-        std::memset(&cp.header, 0, sizeof(cp.header));
-        cp.header.n_template = counter;
-        std::snprintf(cp.header.originalfile, sizeof(cp.header.originalfile), "%s", opt.inputfile.c_str());
-        std::memcpy(cp.cands, table.data(), sizeof(cp.cands));
-        rc = write_checkpoint(opt.checkpointfile, cp);
-        if (rc) break;
-        log_message(LOG_INFO, true, "Checkpoint committed!\n");
-        boinc::checkpoint_completed();
-      }
-      if (kill_after >= 0 && counter >= static_cast<uint32_t>(kill_after)) boinc::request_quit();
-      const boinc::Status st = boinc::get_status();
-      if (st.quit_request || st.abort_request || st.no_heartbeat) quit = true;
-    }
-    if (rc) break;
-    applied = br.first + static_cast<uint32_t>(br.cands.size());
-    {
-      std::lock_guard<std::mutex> lk(mu);
-      table.thresholds(g.chi2_thr, thr_shared);
-    }
-  }
-  stop.store(true);
-  for (auto& th : threads) th.join();
+    if (kill_after >= 0 && counter >= static_cast<uint32_t>(kill_after)) boinc::request_quit();
+    const boinc::Status st = boinc::get_status();
+    return !(st.quit_request || st.abort_request || st.no_heartbeat);
+  };
+  rc = session.run(begin, end, table, res, hook);
   res.t_templates = now_s() - t_loop;
   res.templates_done = counter;
-  for (auto& be : backends) {
-    const BackendStats s = be->stats();
-    res.stats.gpu_ms += s.gpu_ms;
-    res.stats.whiten_ms += s.whiten_ms;
-    res.stats.templates += s.templates;
-    res.stats.batches += s.batches;
-    res.stats.overflow_reruns += s.overflow_reruns;
-  }
+  res.stats = session.stats();
   if (rc) return rc;
-  if (quit) {
-    res.interrupted = true;
+  if (cp_rc) return cp_rc;
+  if (res.interrupted) {
+    // the reference exits without a final checkpoint (demod_binary.c:1489-1492)
     log_message(LOG_WARN, true, "BOINC wants us to quit prematurely or we lost contact! Exiting...\n");
     res.t_total = now_s() - t_start;
     return 0;

@@ -3,9 +3,11 @@
 
 #include <cstdint>
 #include <functional>
+#include <memory>
 #include <string>
 #include <vector>
 
+#include "../core/io.hpp"
 #include "../core/search_core.hpp"
 #include "../engine/backend.hpp"
 
@@ -32,6 +34,33 @@ struct SearchControl {
   std::vector<int> devices;       // explicit device ids (optional)
   // called after every template applied (progress hooks / fault injection)
   std::function<void(uint32_t done, uint32_t total)> on_template;
+};
+
+// Per-template hook of SearchSession::run: return false to stop after this template.
+using TemplateHook = std::function<bool(uint32_t done, const SearchInfo& info)>;
+
+// One work unit held open: bank, series, geometry and the device backends.
+// Reused across runs (benchmark steps, sharded ranges) without re-reading files.
+class SearchSession {
+ public:
+  SearchSession();
+  ~SearchSession();
+  // read bank / WU / zaplist and create the backends (no device work yet)
+  int open(const SearchOptions& opt, const SearchControl& ctl);
+  // (re)upload the raw series and whiten it on the device(s); required before run()
+  int prepare();
+  // process templates [begin, end) and apply them in template order to `table`
+  int run(uint32_t begin, uint32_t end, CandidateTable& table, SearchResult& res, const TemplateHook& hook);
+  const SearchGeometry& geometry() const;
+  const TemplateBank& bank() const;
+  const WorkUnit& work_unit() const;
+  const SearchOptions& options() const;
+  uint32_t total() const;
+  BackendStats stats() const;
+
+ private:
+  struct Impl;
+  std::unique_ptr<Impl> impl_;
 };
 
 // Full search of one WU with the options' files. Returns a RADPUL_* code.

@@ -470,6 +470,54 @@ PYBIND11_MODULE(_brp, m) {
       },
       py::arg("options"), py::arg("begin") = 0, py::arg("end") = 0, py::arg("write_output") = true,
       py::arg("use_checkpoint") = true, py::arg("gpus") = 1);
+  py::class_<SearchSession>(m, "SearchSession")
+      .def(py::init<>())
+      .def(
+          "open",
+          [](SearchSession& s, const py::dict& od, int gpus, std::vector<int> devices) {
+            SearchControl ctl;
+            ctl.gpus = gpus;
+            ctl.devices = devices;
+            check(s.open(dict_to_options(od), ctl), "SearchSession.open");
+          },
+          py::arg("options"), py::arg("gpus") = 1, py::arg("devices") = std::vector<int>())
+      .def("prepare",
+           [](SearchSession& s) {
+             int rc;
+             {
+               py::gil_scoped_release rel;
+               rc = s.prepare();
+             }
+             check(rc, "SearchSession.prepare");
+           })
+      .def(
+          "run",
+          [](SearchSession& s, uint32_t begin, uint32_t end, CandidateTable table) {
+            SearchResult res;
+            int rc;
+            {
+              py::gil_scoped_release rel;
+              rc = s.run(begin, end, table, res, nullptr);
+            }
+            check(rc, "SearchSession.run");
+            py::dict d;
+            d["templates_run"] = res.templates_run;
+            d["dirty_pages"] = res.dirty_pages;
+            return py::make_tuple(table, d);
+          },
+          py::arg("begin"), py::arg("end"), py::arg("table") = CandidateTable())
+      .def("geometry", [](SearchSession& s) { return geometry_to_dict(s.geometry()); })
+      .def("total", &SearchSession::total)
+      .def("stats", [](SearchSession& s) {
+        const BackendStats st = s.stats();
+        py::dict d;
+        d["gpu_ms"] = st.gpu_ms;
+        d["whiten_ms"] = st.whiten_ms;
+        d["templates"] = st.templates;
+        d["batches"] = st.batches;
+        d["overflow_reruns"] = st.overflow_reruns;
+        return d;
+      });
   m.def("finalize_output", [](const py::dict& od, const py::dict& gd, uint32_t n_done, CandidateTable t) {
     check(finalize_output(dict_to_options(od), dict_to_geometry(gd), n_done, t, "einsteinbinary_mi355x"),
           "finalize_output");
