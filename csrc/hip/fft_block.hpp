@@ -137,11 +137,22 @@ struct Dft<16> {
 };
 
 // ------------------------------------------------------------ block FFT core
+// Row layout: one pad element every 16 (r + r/16) and a row pitch == 16 (mod 32)
+// keep both the radix-16 scatter (stride-16 writes of a 16-lane group) and the
+// two-row reads of a 32-lane group bank-conflict free.
+template <int L>
+constexpr int row_pitch() {
+  return (L + L / 16) + ((16 - (L + L / 16) % 32) + 32) % 32;
+}
+
 template <int L, int NCOL, int TPC, bool ROWMAJOR>
 struct BlockLayout {
   static constexpr int kThreads = NCOL * TPC;
-  static constexpr int kLds = ROWMAJOR ? NCOL * (L + 1) : L * NCOL;  // float2 elements
-  __device__ __forceinline__ static int idx(int r, int c) { return ROWMAJOR ? c * (L + 1) + r : r * NCOL + c; }
+  static constexpr int kPitch = row_pitch<L>();
+  static constexpr int kLds = ROWMAJOR ? NCOL * kPitch : L * NCOL;  // float2 elements
+  __device__ __forceinline__ static int idx(int r, int c) {
+    return ROWMAJOR ? c * kPitch + r + (r >> 4) : r * NCOL + c;
+  }
   __device__ __forceinline__ static void coords(int tid, int& c, int& tj) {
     if (ROWMAJOR) {
       tj = tid % TPC;

@@ -54,10 +54,12 @@ __global__ void __launch_bounds__(kNcol * tpc_for<L>()) pass1_kernel(Pass1Args a
   constexpr int TPC = tpc_for<L>();
   constexpr int NT = kNcol * TPC;
   using Lay = BlockLayout<L, kNcol, TPC, false>;
-  __shared__ __attribute__((aligned(16))) float2 smem[Lay::kLds + L + 16];
+  // data | stage twiddles W_L | output twiddles W_{L1 L2}^{n2 k1} | reduction scratch
+  __shared__ __attribute__((aligned(16))) float2 smem[Lay::kLds + 2 * L + 16];
   float2* data = smem;
   float2* twl = smem + Lay::kLds;
-  double* red = reinterpret_cast<double*>(smem + Lay::kLds + L);
+  float2* two = twl + L;
+  double* red = reinterpret_cast<double*>(two + L);
 
   const int b = blockIdx.y;
   const uint32_t nblk3 = a.L3 / kNcol;
@@ -66,6 +68,8 @@ __global__ void __launch_bounds__(kNcol * tpc_for<L>()) pass1_kernel(Pass1Args a
   const size_t M = static_cast<size_t>(L) * a.L2L3;
 
   load_stage_twiddles<L>(twl, a.tw);
+  const uint32_t tw_step = n2 * 4u * a.L3;  // W_{L1 L2}^{n2 k1} = W_2N^{n2 k1 4 L3}
+  for (int k1 = threadIdx.x; k1 < L; k1 += NT) two[k1] = tw_lookup32(a.tw, tw_step * static_cast<uint32_t>(k1));
   int c, tj;
   Lay::coords(threadIdx.x, c, tj);
 
@@ -97,10 +101,8 @@ __global__ void __launch_bounds__(kNcol * tpc_for<L>()) pass1_kernel(Pass1Args a
   BlockFFT<L, kNcol, TPC, false>::run(data, twl);
 
   float2* out = a.out + static_cast<size_t>(b) * M;
-  const uint32_t tw_step = n2 * 4u * a.L3;  // W_{L1 L2}^{n2 k1} = W_2N^{n2 k1 4 L3}
   for (int k1 = tj; k1 < L; k1 += TPC) {
-    float2 v = data[Lay::idx(k1, c)];
-    v = cmul(v, tw_lookup32(a.tw, tw_step * static_cast<uint32_t>(k1)));
+    const float2 v = cmul(data[Lay::idx(k1, c)], two[k1]);
     out[static_cast<size_t>(k1) * a.L2L3 + col_base + c] = v;
   }
   if (MODE == P1_RESAMPLE) {
@@ -110,13 +112,22 @@ __global__ void __launch_bounds__(kNcol * tpc_for<L>()) pass1_kernel(Pass1Args a
 }
 
 // ------------------------------------------------------------------ pass 2
+constexpr int kP2LoBits = 8;
+
 template <int L>
 __global__ void __launch_bounds__(kNcol * tpc_for<L>()) pass2_kernel(Pass2Args a) {
   constexpr int TPC = tpc_for<L>();
+  constexpr int NT = kNcol * TPC;
   using Lay = BlockLayout<L, kNcol, TPC, false>;
-  __shared__ __attribute__((aligned(16))) float2 smem[Lay::kLds + L];
+  constexpr int kLo = 1 << kP2LoBits;
+  constexpr int kHiMax = 512;  // L2*L3 <= 2^17
+  // data | stage twiddles | column twiddles W_M^{n3 k1} | W_{L2L3} lo | W_{L2L3} hi
+  __shared__ __attribute__((aligned(16))) float2 smem[Lay::kLds + L + kNcol + kLo + kHiMax];
   float2* data = smem;
   float2* twl = smem + Lay::kLds;
+  float2* colw = twl + L;
+  float2* lo = colw + kNcol;
+  float2* hi = lo + kLo;
 
   const int b = blockIdx.y;
   const uint32_t nblk3 = a.L3 / kNcol;
@@ -127,17 +138,22 @@ __global__ void __launch_bounds__(kNcol * tpc_for<L>()) pass2_kernel(Pass2Args a
   const size_t base = static_cast<size_t>(k1) * a.L2L3 + n3_0;
 
   load_stage_twiddles<L>(twl, a.tw);
+  // W_M^{n3 (k1 + L1 k2)} = W_M^{n3 k1} * W_{L2 L3}^{n3 k2};  W_{L2L3}^j = W_2N^{4 L1 j}
+  const uint32_t nhi = (a.L2L3 + kLo - 1) / kLo;
+  for (int i = threadIdx.x; i < kNcol; i += NT) colw[i] = tw_lookup32(a.tw, 4u * (n3_0 + i) * k1);
+  for (int i = threadIdx.x; i < kLo; i += NT) lo[i] = tw_lookup32(a.tw, 4u * a.L1 * static_cast<uint32_t>(i));
+  for (uint32_t i = threadIdx.x; i < nhi; i += NT) hi[i] = tw_lookup32(a.tw, 4u * a.L1 * (i << kP2LoBits));
   int c, tj;
   Lay::coords(threadIdx.x, c, tj);
   for (int r = tj; r < L; r += TPC) data[Lay::idx(r, c)] = buf[base + static_cast<size_t>(r) * a.L3 + c];
   __syncthreads();
   BlockFFT<L, kNcol, TPC, false>::run(data, twl);
   const uint32_t n3 = n3_0 + c;
+  const float2 wc = colw[c];
   for (int k2 = tj; k2 < L; k2 += TPC) {
-    float2 v = data[Lay::idx(k2, c)];
-    // W_M^{n3 (k1 + L1 k2)} = W_2N^{4 n3 (k1 + L1 k2)}
-    v = cmul(v, tw_lookup32(a.tw, 4u * n3 * (k1 + a.L1 * static_cast<uint32_t>(k2))));
-    buf[base + static_cast<size_t>(k2) * a.L3 + c] = v;
+    const uint32_t e = n3 * static_cast<uint32_t>(k2);  // < L2*L3
+    const float2 w = cmul(wc, cmul(hi[e >> kP2LoBits], lo[e & (kLo - 1)]));
+    buf[base + static_cast<size_t>(k2) * a.L3 + c] = cmul(data[Lay::idx(k2, c)], w);
   }
 }
 
@@ -147,23 +163,42 @@ __device__ __forceinline__ size_t row_base(uint32_t c, uint32_t L1, uint32_t L2,
   return (static_cast<size_t>(k1) * L2 + k2) * L3;
 }
 
-// X_k of the real FFT from Z_k and Z_{M-k} of the packed complex FFT.
-__device__ __forceinline__ float2 untangle(float2 zk, float2 zmk, const TwiddleTable& tw, uint32_t k) {
+// X_k of the real FFT from Z_k, Z_{M-k} of the packed complex FFT and w = W_N^k.
+__device__ __forceinline__ float2 untangle_w(float2 zk, float2 zmk, float2 w) {
   const float2 bc = conjf2(zmk);
   const float2 e = cscale(cadd(zk, bc), 0.5f);
   const float2 o = cscale(csub(zk, bc), 0.5f);
-  const float2 w = tw_lookup32(tw, 2u * k);  // W_N^k
   return cadd(e, mul_mi(cmul(w, o)));
 }
 
 // FFT of the padding indicator 1[m >= n_s] (m < N) at bin k in [1, N/2]:
-// S_k = -(sin(pi n_s k / N) / sin(pi k / N)) * exp(-i pi (n_s - 1) k / N)
-__device__ __forceinline__ float2 padding_spectrum(const TwiddleTable& tw, uint32_t n_s, uint32_t k) {
-  const float2 ta = tw_lookup(tw, static_cast<uint64_t>(n_s) * k);
-  const float2 tk = tw_lookup32(tw, k);
-  const float2 tc = tw_lookup(tw, static_cast<uint64_t>(n_s - 1) * k);
+// S_k = -(sin(pi n_s k / N) / sin(pi k / N)) * exp(-i pi (n_s - 1) k / N),
+// from ta = W_2N^{n_s k}, tk = W_2N^k, tc = W_2N^{(n_s-1) k}.
+__device__ __forceinline__ float2 padding_spectrum_t(float2 ta, float2 tk, float2 tc) {
   const float ratio = ta.y / tk.y;
   return make_float2(-ratio * tc.x, -ratio * tc.y);
+}
+
+__device__ __forceinline__ float2 padding_spectrum(const TwiddleTable& tw, uint32_t n_s, uint32_t k) {
+  return padding_spectrum_t(tw_lookup(tw, static_cast<uint64_t>(n_s) * k), tw_lookup32(tw, k),
+                            tw_lookup(tw, static_cast<uint64_t>(n_s - 1) * k));
+}
+
+// Per-row constants: bin k = c + C k3 factors as W_2N^{x k} = W_2N^{x c} * W_{4 L3}^{x k3}
+struct RowTw {
+  float2 w;   // W_N^c       (untangle)
+  float2 t1;  // W_2N^c
+  float2 ta;  // W_2N^{n_s c}
+  float2 tc;  // W_2N^{(n_s-1) c}
+};
+
+__device__ __forceinline__ RowTw row_twiddles(const TwiddleTable& tw, uint32_t c, uint32_t n_s) {
+  RowTw r;
+  r.w = tw_lookup32(tw, 2u * c);
+  r.t1 = tw_lookup32(tw, c);
+  r.ta = tw_lookup(tw, static_cast<uint64_t>(n_s) * c);
+  r.tc = tw_lookup(tw, static_cast<uint64_t>(n_s == 0 ? 0 : n_s - 1) * c);
+  return r;
 }
 
 template <int L, int ROWS, int MODE>
@@ -171,17 +206,21 @@ __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Arg
   constexpr int TPC = tpc_for<L>();
   constexpr int NSLOT = 2 * ROWS;
   constexpr int NT = NSLOT * TPC;
+  constexpr int L4 = 4 * L;
   using Lay = BlockLayout<L, NSLOT, TPC, true>;
-  __shared__ __attribute__((aligned(16))) float2 smem[Lay::kLds + L + 16];
+  // data | stage twiddles W_L | W_{4L} (= W_2N^{C i}) | reduction scratch
+  __shared__ __attribute__((aligned(16))) float2 smem[Lay::kLds + L + L4 + 16];
   float2* data = smem;
   float2* twl = smem + Lay::kLds;
-  double* red = reinterpret_cast<double*>(smem + Lay::kLds + L);
+  float2* t4 = twl + L;
+  double* red = reinterpret_cast<double*>(t4 + L4);
 
   const int b = blockIdx.y;
   const float2* buf = a.buf + static_cast<size_t>(b) * a.M;
   const uint32_t c0 = blockIdx.x * ROWS;
 
   load_stage_twiddles<L>(twl, a.tw);
+  for (int i = threadIdx.x; i < L4; i += NT) t4[i] = tw_lookup32(a.tw, a.C * static_cast<uint32_t>(i));
   {
     int slot, tj;
     Lay::coords(threadIdx.x, slot, tj);
@@ -204,15 +243,19 @@ __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Arg
   __syncthreads();
   BlockFFT<L, NSLOT, TPC, true>::run(data, twl);
 
-  const float2 dS = make_float2(static_cast<float>(delta), 0.0f);
-  auto emit = [&](uint32_t k, float2 x) {
+  const float dS = static_cast<float>(delta);
+  const bool correct = (MODE == P3_POWER) && n_s > 0;
+  auto emit = [&](uint32_t k, float2 x, const RowTw& rt, uint32_t k3) {
     if (k >= a.limit) return;
     if (MODE == P3_POWER) {
       float p = 0.0f;
       if (k != 0) {
-        if (n_s > 0) {
-          const float2 s = padding_spectrum(a.tw, n_s, k);
-          x = make_float2(x.x + dS.x * s.x, x.y + dS.x * s.y);
+        if (correct) {
+          const float2 ta = cmul(rt.ta, t4[(n_s * k3) % L4]);
+          const float2 tk = cmul(rt.t1, t4[k3]);
+          const float2 tc = cmul(rt.tc, t4[((n_s - 1) * k3) % L4]);
+          const float2 s = padding_spectrum_t(ta, tk, tc);
+          x = make_float2(x.x + dS * s.x, x.y + dS * s.y);
         }
         const double re = x.x, im = x.y;
         p = static_cast<float>(static_cast<double>(a.norm) * (re * re + im * im));
@@ -230,23 +273,35 @@ __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Arg
   const uint32_t c = c0 + s;
   const uint32_t half = a.C / 2;
   if (c <= half) {
+    const uint32_t cm = (a.C - c) % a.C;
+    const RowTw rt = row_twiddles(a.tw, c, n_s);
+    const RowTw rm = row_twiddles(a.tw, cm, n_s);
     for (int k3 = t; k3 < L; k3 += kStreams) {
       const float2 zk = data[Lay::idx(k3, s)];
-      float2 zm;
-      if (c == 0) {
-        zm = data[Lay::idx((L - k3) % L, s)];
-      } else {
-        zm = data[Lay::idx(L - 1 - k3, ROWS + s)];
-      }
+      const int k3m = (c == 0) ? (L - k3) % L : L - 1 - k3;
+      const float2 zm = data[Lay::idx(k3m, c == 0 ? s : ROWS + s)];
       const uint32_t k = c + a.C * static_cast<uint32_t>(k3);
-      emit(k, untangle(zk, zm, a.tw, k));
+      const float2 w = cmul(rt.w, t4[(2 * k3) % L4]);  // W_N^k
+      emit(k, untangle_w(zk, zm, w), rt, static_cast<uint32_t>(k3));
       if (c != 0 && c != half) {
-        const uint32_t kk = a.M - k;
-        emit(kk, untangle(zm, zk, a.tw, kk));
+        const uint32_t kk = a.M - k;  // = cm + C*(L-1-k3)
+        const float2 wm = make_float2(-w.x, w.y);  // W_N^{M-k} = -conj(W_N^k)
+        emit(kk, untangle_w(zm, zk, wm), rm, static_cast<uint32_t>(L - 1 - k3));
       }
-      if (c == 0 && k3 == 0) {
+      if (c == 0 && k3 == 0 && a.M < a.limit) {
         // Nyquist bin M: X_M = Re Z_0 - Im Z_0
-        emit(a.M, make_float2(zk.x - zk.y, 0.0f));
+        float2 x = make_float2(zk.x - zk.y, 0.0f);
+        if (MODE == P3_POWER) {
+          if (correct) {
+            const float2 sp = padding_spectrum(a.tw, n_s, a.M);
+            x = make_float2(x.x + dS * sp.x, x.y + dS * sp.y);
+          }
+          const double re = x.x, im = x.y;
+          a.ps[static_cast<size_t>(b) * a.ps_stride + a.M] =
+              static_cast<float>(static_cast<double>(a.norm) * (re * re + im * im));
+        } else {
+          a.spec[a.M] = x;
+        }
       }
     }
   }
