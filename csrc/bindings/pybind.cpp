@@ -415,6 +415,19 @@ PYBIND11_MODULE(_brp, m) {
              check(e.power_spectrum(TemplateInput{P, tau, psi}, ps, &n_steps), "HipEngine.power_spectrum");
              return py::make_tuple(py::array_t<float>(ps.size(), ps.data()), n_steps);
            })
+      .def("benchmark_stages",
+           [](HipEngine& e, py::array_t<float> P, py::array_t<float> tau, py::array_t<float> psi, int reps) {
+             auto t = arrays_to_templates(P, tau, psi);
+             std::vector<double> us;
+             {
+               py::gil_scoped_release rel;
+               check(e.benchmark_stages(t.data(), static_cast<int>(t.size()), reps, us), "benchmark_stages");
+             }
+             py::dict d;
+             const char* names[] = {"prologue", "pass1", "pass2", "pass3", "harmonic", "epilogue", "batch"};
+             for (size_t i = 0; i < us.size(); ++i) d[names[i]] = us[i];
+             return d;
+           })
       .def("plan",
            [](HipEngine& e) {
              const FFTPlan3& p = e.plan();

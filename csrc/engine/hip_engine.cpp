@@ -125,6 +125,20 @@ void build_twiddles(uint64_t period, std::vector<float2>& hi, std::vector<float2
   for (uint32_t j = 0; j < nlo; ++j) lo[j] = w(j);
 }
 
+// exp(-2 pi i num/den) with exact integer reduction
+float2 root(uint64_t num, uint64_t den) {
+  num %= den;
+  const long double pi = 3.14159265358979323846264338327950288L;
+  const long double a = -2.0L * pi * static_cast<long double>(num) / static_cast<long double>(den);
+  return make_float2(static_cast<float>(cosl(a)), static_cast<float>(sinl(a)));
+}
+
+std::vector<float2> stage_table(uint32_t L) {
+  std::vector<float2> t(L + L / 16 + 1, make_float2(0.f, 0.f));
+  for (uint32_t e = 0; e < L; ++e) t[e + (e >> 4)] = root(e, L);
+  return t;
+}
+
 }  // namespace
 
 struct HipEngine::Impl {
@@ -151,6 +165,7 @@ struct HipEngine::Impl {
   DevBuf<uint32_t> counts;      // [batch][5]
   DevBuf<uint2> cands;          // [batch][5][cap]
   DevBuf<float2> tw_hi, tw_lo;
+  DevBuf<float2> t_st1, t_st2, t_st3, t_p1, t_p2col, t_p2lo, t_p2hi, t_p3;
 
   PinnedBuf<TemplateDev> h_tmpl;
   PinnedBuf<float> h_thr;
@@ -159,6 +174,54 @@ struct HipEngine::Impl {
 
   std::map<int, hipGraphExec_t> graphs;
   BackendStats st;
+
+  hipk::FFTTables tables() const {
+    hipk::FFTTables t;
+    t.st1 = t_st1.p;
+    t.st2 = t_st2.p;
+    t.st3 = t_st3.p;
+    t.p1 = t_p1.p;
+    t.p2col = t_p2col.p;
+    t.p2lo = t_p2lo.p;
+    t.p2hi = t_p2hi.p;
+    t.p3 = t_p3.p;
+    return t;
+  }
+
+  int upload(DevBuf<float2>& d, const std::vector<float2>& h) {
+    int rc = d.alloc(h.size());
+    if (rc) return rc;
+    if (hipMemcpy(d.p, h.data(), h.size() * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess)
+      return RADPUL_HIP_MEM_COPY_HOST_DEVICE;
+    return 0;
+  }
+
+  int build_tables() {
+    const uint32_t L1 = plan.L1, L2 = plan.L2, L3 = plan.L3, M = plan.M;
+    const uint64_t L2L3 = static_cast<uint64_t>(L2) * L3;
+    std::vector<float2> v;
+    int rc;
+    if ((rc = upload(t_st1, stage_table(L1)))) return rc;
+    if ((rc = upload(t_st2, stage_table(L2)))) return rc;
+    if ((rc = upload(t_st3, stage_table(L3)))) return rc;
+    v.resize(static_cast<size_t>(L2) * L1);
+    for (uint32_t n2 = 0; n2 < L2; ++n2)
+      for (uint32_t k1 = 0; k1 < L1; ++k1) v[n2 * L1 + k1] = root(static_cast<uint64_t>(n2) * k1, static_cast<uint64_t>(L1) * L2);
+    if ((rc = upload(t_p1, v))) return rc;
+    v.assign(static_cast<size_t>(L1) * L3, make_float2(0, 0));
+    for (uint32_t k1 = 0; k1 < L1; ++k1)
+      for (uint32_t n3 = 0; n3 < L3; ++n3) v[k1 * L3 + n3] = root(static_cast<uint64_t>(n3) * k1, M);
+    if ((rc = upload(t_p2col, v))) return rc;
+    v.assign(256, make_float2(0, 0));
+    for (uint32_t i = 0; i < 256; ++i) v[i] = root(i, L2L3);
+    if ((rc = upload(t_p2lo, v))) return rc;
+    v.assign(512, make_float2(0, 0));
+    for (uint32_t i = 0; i < 512 && 256ull * i < L2L3; ++i) v[i] = root(256ull * i, L2L3);
+    if ((rc = upload(t_p2hi, v))) return rc;
+    v.assign(4ull * L3, make_float2(0, 0));
+    for (uint32_t i = 0; i < 4 * L3; ++i) v[i] = root(i, 4ull * L3);
+    return upload(t_p3, v);
+  }
 
   hipk::TwiddleTable twt() const {
     hipk::TwiddleTable t;
@@ -175,73 +238,95 @@ struct HipEngine::Impl {
     if (stream) (void)hipStreamDestroy(stream);
   }
 
+  // Pipeline stages of one batch; the whole sequence is captured into a graph.
+  enum Stage { kPrologue = 0, kPass1, kPass2, kPass3, kHarmonic, kEpilogue, kNumStages };
+
+  hipError_t enqueue_stage(int st, int nb) {
+    hipError_t e = hipSuccess;
+    const hipk::TwiddleTable tw = twt();
+    switch (st) {
+      case kPrologue:
+        e = hipMemcpyAsync(tmpl.p, h_tmpl.p, sizeof(TemplateDev) * nb, hipMemcpyHostToDevice, stream);
+        if (e != hipSuccess) return e;
+        e = hipMemcpyAsync(thr.p, h_thr.p, sizeof(float) * kNumHarmonicLevels, hipMemcpyHostToDevice, stream);
+        if (e != hipSuccess) return e;
+        e = hipMemsetAsync(counts.p, 0, sizeof(uint32_t) * kNumHarmonicLevels * nb, stream);
+        if (e != hipSuccess) return e;
+        return hipk::launch_nsteps(tmpl.p, nb, stream);
+      case kPass1: {
+        hipk::Pass1Args a1{};
+        a1.out = buf.p;
+        a1.L2L3 = plan.L2 * plan.L3;
+        a1.L3 = plan.L3;
+        a1.tw = tw;
+        a1.tb = tables();
+        a1.series = series.p;
+        a1.n_unpadded = g.n_unpadded;
+        a1.tmpl = tmpl.p;
+        a1.partials = partials.p;
+        return hipk::launch_pass1(plan, hipk::P1_RESAMPLE, a1, nb, stream);
+      }
+      case kPass2: {
+        hipk::Pass2Args a2{};
+        a2.buf = buf.p;
+        a2.L1 = plan.L1;
+        a2.L2L3 = plan.L2 * plan.L3;
+        a2.L3 = plan.L3;
+        a2.tw = tw;
+        a2.tb = tables();
+        return hipk::launch_pass2(plan, a2, nb, stream);
+      }
+      case kPass3: {
+        hipk::Pass3Args a3{};
+        a3.buf = buf.p;
+        a3.L1 = plan.L1;
+        a3.L2 = plan.L2;
+        a3.L3 = plan.L3;
+        a3.C = plan.L1 * plan.L2;
+        a3.M = plan.M;
+        a3.tw = tw;
+        a3.tb = tables();
+        a3.limit = std::min(g.harmonic_idx_hi, g.fft_size);
+        a3.ps = ps.p;
+        a3.ps_stride = ps_stride;
+        a3.norm = static_cast<float>(1.0 / g.nsamples);
+        a3.tmpl = tmpl.p;
+        a3.partials = partials.p;
+        a3.n_partials = plan.wg1();
+        return hipk::launch_pass3(plan, hipk::P3_POWER, a3, nb, stream);
+      }
+      case kHarmonic: {
+        hipk::HSArgs ah{};
+        ah.ps = ps.p;
+        ah.ps_stride = ps_stride;
+        ah.w2 = g.window_2;
+        ah.fhi = g.fundamental_idx_hi;
+        ah.hhi = std::min(g.harmonic_idx_hi, g.fft_size);
+        ah.i_start = i_start;
+        ah.thr = thr.p;
+        ah.counts = counts.p;
+        ah.cands = cands.p;
+        ah.cap = cap;
+        return hipk::launch_harmonic_sum(ah, nb, stream);
+      }
+      case kEpilogue:
+        e = hipMemcpyAsync(h_counts.p, counts.p, sizeof(uint32_t) * kNumHarmonicLevels * nb, hipMemcpyDeviceToHost,
+                           stream);
+        if (e != hipSuccess) return e;
+        return hipMemcpy2DAsync(h_cands.p, sizeof(uint2) * kcopy, cands.p, sizeof(uint2) * cap,
+                                sizeof(uint2) * kcopy, static_cast<size_t>(kNumHarmonicLevels) * nb,
+                                hipMemcpyDeviceToHost, stream);
+      default: return hipErrorInvalidValue;
+    }
+  }
+
   // Enqueue the whole per-batch pipeline on `stream` (also used for capture).
   hipError_t enqueue(int nb) {
-    hipError_t e;
-    e = hipMemcpyAsync(tmpl.p, h_tmpl.p, sizeof(TemplateDev) * nb, hipMemcpyHostToDevice, stream);
-    if (e != hipSuccess) return e;
-    e = hipMemcpyAsync(thr.p, h_thr.p, sizeof(float) * kNumHarmonicLevels, hipMemcpyHostToDevice, stream);
-    if (e != hipSuccess) return e;
-    e = hipMemsetAsync(counts.p, 0, sizeof(uint32_t) * kNumHarmonicLevels * nb, stream);
-    if (e != hipSuccess) return e;
-    e = hipk::launch_nsteps(tmpl.p, nb, stream);
-    if (e != hipSuccess) return e;
-    const hipk::TwiddleTable tw = twt();
-    hipk::Pass1Args a1{};
-    a1.out = buf.p;
-    a1.L2L3 = plan.L2 * plan.L3;
-    a1.L3 = plan.L3;
-    a1.tw = tw;
-    a1.series = series.p;
-    a1.n_unpadded = g.n_unpadded;
-    a1.tmpl = tmpl.p;
-    a1.partials = partials.p;
-    e = hipk::launch_pass1(plan, hipk::P1_RESAMPLE, a1, nb, stream);
-    if (e != hipSuccess) return e;
-    hipk::Pass2Args a2{};
-    a2.buf = buf.p;
-    a2.L1 = plan.L1;
-    a2.L2L3 = plan.L2 * plan.L3;
-    a2.L3 = plan.L3;
-    a2.tw = tw;
-    e = hipk::launch_pass2(plan, a2, nb, stream);
-    if (e != hipSuccess) return e;
-    hipk::Pass3Args a3{};
-    a3.buf = buf.p;
-    a3.L1 = plan.L1;
-    a3.L2 = plan.L2;
-    a3.L3 = plan.L3;
-    a3.C = plan.L1 * plan.L2;
-    a3.M = plan.M;
-    a3.tw = tw;
-    a3.limit = std::min(g.harmonic_idx_hi, g.fft_size);
-    a3.ps = ps.p;
-    a3.ps_stride = ps_stride;
-    a3.norm = static_cast<float>(1.0 / g.nsamples);
-    a3.tmpl = tmpl.p;
-    a3.partials = partials.p;
-    a3.n_partials = plan.wg1();
-    e = hipk::launch_pass3(plan, hipk::P3_POWER, a3, nb, stream);
-    if (e != hipSuccess) return e;
-    hipk::HSArgs ah{};
-    ah.ps = ps.p;
-    ah.ps_stride = ps_stride;
-    ah.w2 = g.window_2;
-    ah.fhi = g.fundamental_idx_hi;
-    ah.hhi = std::min(g.harmonic_idx_hi, g.fft_size);
-    ah.i_start = i_start;
-    ah.thr = thr.p;
-    ah.counts = counts.p;
-    ah.cands = cands.p;
-    ah.cap = cap;
-    e = hipk::launch_harmonic_sum(ah, nb, stream);
-    if (e != hipSuccess) return e;
-    e = hipMemcpyAsync(h_counts.p, counts.p, sizeof(uint32_t) * kNumHarmonicLevels * nb, hipMemcpyDeviceToHost,
-                       stream);
-    if (e != hipSuccess) return e;
-    e = hipMemcpy2DAsync(h_cands.p, sizeof(uint2) * kcopy, cands.p, sizeof(uint2) * cap, sizeof(uint2) * kcopy,
-                         static_cast<size_t>(kNumHarmonicLevels) * nb, hipMemcpyDeviceToHost, stream);
-    return e;
+    for (int st = 0; st < kNumStages; ++st) {
+      const hipError_t e = enqueue_stage(st, nb);
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
   }
 };
 
@@ -318,6 +403,7 @@ int HipEngine::setup(const SearchGeometry& g, const std::vector<float>& series, 
                 RADPUL_HIP_MEM_COPY_HOST_DEVICE);
   BRP_HIP_CHECK(hipMemcpy(d.tw_lo.p, lo.data(), lo.size() * sizeof(float2), hipMemcpyHostToDevice),
                 RADPUL_HIP_MEM_COPY_HOST_DEVICE);
+  if ((rc = d.build_tables())) return rc;
   BRP_HIP_CHECK(hipMemcpy(d.series.p, series.data(), g.n_unpadded * sizeof(float), hipMemcpyHostToDevice),
                 RADPUL_HIP_MEM_COPY_HOST_DEVICE);
   d.ready = true;
@@ -357,6 +443,7 @@ int HipEngine::whiten(const SearchOptions& opt, const std::vector<ZapRange>& zap
   a1.L2L3 = d.plan.L2 * d.plan.L3;
   a1.L3 = d.plan.L3;
   a1.tw = tw;
+  a1.tb = d.tables();
   a1.real_in = d.series.p;
   a1.n_real = g.n_unpadded;
   BRP_HIP_CHECK(hipk::launch_pass1(d.plan, hipk::P1_REAL, a1, 1, s), RADPUL_HIP_KERNEL_INVOKE);
@@ -366,6 +453,7 @@ int HipEngine::whiten(const SearchOptions& opt, const std::vector<ZapRange>& zap
   a2.L2L3 = d.plan.L2 * d.plan.L3;
   a2.L3 = d.plan.L3;
   a2.tw = tw;
+  a2.tb = d.tables();
   BRP_HIP_CHECK(hipk::launch_pass2(d.plan, a2, 1, s), RADPUL_HIP_KERNEL_INVOKE);
   hipk::Pass3Args a3{};
   a3.buf = work;
@@ -375,6 +463,7 @@ int HipEngine::whiten(const SearchOptions& opt, const std::vector<ZapRange>& zap
   a3.C = d.plan.L1 * d.plan.L2;
   a3.M = M;
   a3.tw = tw;
+  a3.tb = d.tables();
   a3.limit = fft_size;
   a3.spec = spec.p;
   BRP_HIP_CHECK(hipk::launch_pass3(d.plan, hipk::P3_COMPLEX, a3, 1, s), RADPUL_HIP_KERNEL_INVOKE);
@@ -418,6 +507,7 @@ int HipEngine::whiten(const SearchOptions& opt, const std::vector<ZapRange>& zap
   a1.L2L3 = d.plan.L2 * d.plan.L3;
   a1.L3 = d.plan.L3;
   a1.tw = tw;
+  a1.tb = d.tables();
   a1.cplx_in = z.p;
   BRP_HIP_CHECK(hipk::launch_pass1(d.plan, hipk::P1_COMPLEX_CONJ, a1, 1, s), RADPUL_HIP_KERNEL_INVOKE);
   BRP_HIP_CHECK(hipk::launch_pass2(d.plan, a2, 1, s), RADPUL_HIP_KERNEL_INVOKE);
@@ -428,6 +518,7 @@ int HipEngine::whiten(const SearchOptions& opt, const std::vector<ZapRange>& zap
   ap.L3 = d.plan.L3;
   ap.C = d.plan.L1 * d.plan.L2;
   ap.tw = tw;
+  ap.tb = d.tables();
   ap.scale = static_cast<float>(1.0 / std::sqrt(static_cast<float>(g.nsamples)));
   ap.real_out = d.series.p;
   ap.n_out = g.n_unpadded;
@@ -542,6 +633,7 @@ int HipEngine::power_spectrum(const TemplateInput& t, std::vector<float>& ps_out
   a1.L2L3 = d.plan.L2 * d.plan.L3;
   a1.L3 = d.plan.L3;
   a1.tw = tw;
+  a1.tb = d.tables();
   a1.series = d.series.p;
   a1.n_unpadded = g.n_unpadded;
   a1.tmpl = d.tmpl.p;
@@ -553,6 +645,7 @@ int HipEngine::power_spectrum(const TemplateInput& t, std::vector<float>& ps_out
   a2.L2L3 = d.plan.L2 * d.plan.L3;
   a2.L3 = d.plan.L3;
   a2.tw = tw;
+  a2.tb = d.tables();
   BRP_HIP_CHECK(hipk::launch_pass2(d.plan, a2, 1, s), RADPUL_HIP_KERNEL_INVOKE);
   DevBuf<float> full;
   int rc;
@@ -565,6 +658,7 @@ int HipEngine::power_spectrum(const TemplateInput& t, std::vector<float>& ps_out
   a3.C = d.plan.L1 * d.plan.L2;
   a3.M = d.plan.M;
   a3.tw = tw;
+  a3.tb = d.tables();
   a3.limit = g.fft_size;
   a3.ps = full.p;
   a3.ps_stride = g.fft_size;
@@ -580,6 +674,40 @@ int HipEngine::power_spectrum(const TemplateInput& t, std::vector<float>& ps_out
                 RADPUL_HIP_MEM_COPY_DEVICE_HOST);
   BRP_HIP_CHECK(hipStreamSynchronize(s), RADPUL_HIP_KERNEL_INVOKE);
   if (n_steps) *n_steps = d.h_tmpl.p[0].n_steps;
+  return 0;
+}
+
+int HipEngine::benchmark_stages(const TemplateInput* t, int n, int reps, std::vector<double>& us_per_launch) {
+  Impl& d = *impl_;
+  if (!d.ready) return RADPUL_EMISC;
+  const int nb = std::min(n, d.batch);
+  const SearchGeometry& g = d.g;
+  for (int k = 0; k < nb; ++k) {
+    TemplateDev td{};
+    td.p = make_resamp_params(g.nsamples, g.n_unpadded, g.fft_size, g.dt, g.step_inv, t[k].P, t[k].tau, t[k].Psi0);
+    td.mu0 = d.mu0;
+    d.h_tmpl.p[k] = td;
+  }
+  for (int h = 0; h < kNumHarmonicLevels; ++h) d.h_thr.p[h] = d.g.chi2_thr[h];
+  BRP_HIP_CHECK(d.enqueue(nb), RADPUL_HIP_KERNEL_INVOKE);
+  BRP_HIP_CHECK(hipStreamSynchronize(d.stream), RADPUL_HIP_KERNEL_INVOKE);
+  us_per_launch.assign(Impl::kNumStages + 1, 0.0);
+  for (int st = 0; st <= Impl::kNumStages; ++st) {
+    // st == kNumStages: the whole pipeline
+    BRP_HIP_CHECK(hipEventRecord(d.ev0, d.stream), RADPUL_HIP_KERNEL_INVOKE);
+    for (int r = 0; r < reps; ++r) {
+      if (st == Impl::kNumStages) {
+        BRP_HIP_CHECK(d.enqueue(nb), RADPUL_HIP_KERNEL_INVOKE);
+      } else {
+        BRP_HIP_CHECK(d.enqueue_stage(st, nb), RADPUL_HIP_KERNEL_INVOKE);
+      }
+    }
+    BRP_HIP_CHECK(hipEventRecord(d.ev1, d.stream), RADPUL_HIP_KERNEL_INVOKE);
+    BRP_HIP_CHECK(hipStreamSynchronize(d.stream), RADPUL_HIP_KERNEL_INVOKE);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, d.ev0, d.ev1);
+    us_per_launch[st] = 1e3 * ms / reps;
+  }
   return 0;
 }
 

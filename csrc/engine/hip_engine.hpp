@@ -27,6 +27,9 @@ class HipEngine {
   int process(const TemplateInput* t, int n, const float thr[kNumHarmonicLevels], std::vector<TemplateCands>& out);
   // test hooks
   int power_spectrum(const TemplateInput& t, std::vector<float>& ps, uint32_t* n_steps);
+  // time each pipeline stage (prologue, pass1, pass2, pass3, harmonic, epilogue,
+  // whole batch) over `reps` back-to-back launches on one batch; microseconds
+  int benchmark_stages(const TemplateInput* t, int n, int reps, std::vector<double>& us_per_launch);
 
   BackendStats stats() const;
   int device() const;

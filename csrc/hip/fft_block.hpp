@@ -182,7 +182,10 @@ __device__ __forceinline__ void block_stage(float2* lds, const float2* tw_lds) {
       if (Ns > 1) {
         const int jm = j % Ns;
 #pragma unroll
-        for (int q = 1; q < R; ++q) v[u][q] = cmul(v[u][q], tw_lds[(jm * q * (L / (Ns * R))) % L]);
+        for (int q = 1; q < R; ++q) {
+          const int e = (jm * q * (L / (Ns * R))) % L;
+          v[u][q] = cmul(v[u][q], tw_lds[e + (e >> 4)]);  // padded: stride-q reads hit distinct banks
+        }
       }
       Dft<R>::run(v[u]);
     }
@@ -259,12 +262,15 @@ struct BlockFFT {
   }
 };
 
-// Fill a per-length twiddle table W_L^e (e < L) in LDS from the global table
-// W_{2N} (2N multiple of L).
+// Stage twiddle table W_L^e (e < L) stored at e + e/16 (kTwPad<L> entries) so the
+// stride-q reads of a radix-16 stage do not collide on LDS banks. The host
+// precomputes it in exactly this order; kernels copy it contiguously to LDS.
 template <int L>
-__device__ __forceinline__ void load_stage_twiddles(float2* tw_lds, const TwiddleTable& t) {
-  const uint32_t step = static_cast<uint32_t>(t.period / L);
-  for (int e = threadIdx.x; e < L; e += blockDim.x) tw_lds[e] = tw_lookup32(t, static_cast<uint32_t>(e) * step);
+constexpr int kTwPad = L + L / 16 + 1;
+
+template <int L>
+__device__ __forceinline__ void copy_stage_twiddles(float2* tw_lds, const float2* __restrict__ st) {
+  for (int e = threadIdx.x; e < kTwPad<L>; e += blockDim.x) tw_lds[e] = st[e];
 }
 
 }  // namespace hipk

@@ -21,6 +21,20 @@ struct TemplateDev {
   uint32_t pad[2];
 };
 
+// Twiddle tables precomputed on the host per FFT plan (single rounding from
+// double precision; loaded contiguously by the kernels instead of being
+// assembled per element).
+struct FFTTables {
+  const float2* st1;    // stage table W_L1^e, padded order e + e/16
+  const float2* st2;    // stage table W_L2^e
+  const float2* st3;    // stage table W_L3^e
+  const float2* p1;     // [L2][L1]  W_{L1 L2}^{n2 k1}
+  const float2* p2col;  // [L1][L3]  W_M^{n3 k1}
+  const float2* p2lo;   // [256]     W_{L2 L3}^{i}
+  const float2* p2hi;   // [<=512]   W_{L2 L3}^{256 i}
+  const float2* p3;     // [4 L3]    W_2N^{C i}
+};
+
 enum Pass1Mode : int {
   P1_RESAMPLE = 0,   // fused nearest-neighbour resampling of the time series
   P1_REAL = 1,       // zero-padded real series
@@ -31,6 +45,7 @@ struct Pass1Args {
   float2* out;                 // [batch][M]
   uint32_t L2L3, L3;
   TwiddleTable tw;
+  FFTTables tb;
   // P1_RESAMPLE
   const float* series;         // n_unpadded samples (shared by the batch)
   uint32_t n_unpadded;
@@ -47,6 +62,7 @@ struct Pass2Args {
   float2* buf;                 // [batch][M], in place
   uint32_t L1, L2L3, L3;
   TwiddleTable tw;
+  FFTTables tb;
 };
 
 enum Pass3Mode : int {
@@ -59,6 +75,7 @@ struct Pass3Args {
   uint32_t L1, L2, L3, C;      // C = L1*L2 rows
   uint32_t M;
   TwiddleTable tw;
+  FFTTables tb;
   uint32_t limit;              // write bins k < limit only
   // P3_POWER
   float* ps;                   // [batch][ps_stride]
@@ -77,6 +94,7 @@ struct Pass3PlainArgs {
   const float2* buf;
   uint32_t L1, L2, L3, C;
   TwiddleTable tw;
+  FFTTables tb;
   float scale;
   float* real_out;
   uint32_t n_out;              // real samples to write

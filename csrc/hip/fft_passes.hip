@@ -55,10 +55,10 @@ __global__ void __launch_bounds__(kNcol * tpc_for<L>()) pass1_kernel(Pass1Args a
   constexpr int NT = kNcol * TPC;
   using Lay = BlockLayout<L, kNcol, TPC, false>;
   // data | stage twiddles W_L | output twiddles W_{L1 L2}^{n2 k1} | reduction scratch
-  __shared__ __attribute__((aligned(16))) float2 smem[Lay::kLds + 2 * L + 16];
+  __shared__ __attribute__((aligned(16))) float2 smem[Lay::kLds + kTwPad<L> + L + 16];
   float2* data = smem;
   float2* twl = smem + Lay::kLds;
-  float2* two = twl + L;
+  float2* two = twl + kTwPad<L>;
   double* red = reinterpret_cast<double*>(two + L);
 
   const int b = blockIdx.y;
@@ -67,9 +67,6 @@ __global__ void __launch_bounds__(kNcol * tpc_for<L>()) pass1_kernel(Pass1Args a
   const uint32_t col_base = n2 * a.L3 + (blockIdx.x % nblk3) * kNcol;
   const size_t M = static_cast<size_t>(L) * a.L2L3;
 
-  load_stage_twiddles<L>(twl, a.tw);
-  const uint32_t tw_step = n2 * 4u * a.L3;  // W_{L1 L2}^{n2 k1} = W_2N^{n2 k1 4 L3}
-  for (int k1 = threadIdx.x; k1 < L; k1 += NT) two[k1] = tw_lookup32(a.tw, tw_step * static_cast<uint32_t>(k1));
   int c, tj;
   Lay::coords(threadIdx.x, c, tj);
 
@@ -97,6 +94,8 @@ __global__ void __launch_bounds__(kNcol * tpc_for<L>()) pass1_kernel(Pass1Args a
       data[Lay::idx(r, c)] = conjf2(a.cplx_in[static_cast<size_t>(b) * M + n]);
     }
   }
+  copy_stage_twiddles<L>(twl, a.tb.st1);
+  for (int k1 = threadIdx.x; k1 < L; k1 += NT) two[k1] = a.tb.p1[n2 * L + k1];  // W_{L1 L2}^{n2 k1}
   __syncthreads();
   BlockFFT<L, kNcol, TPC, false>::run(data, twl);
 
@@ -122,10 +121,10 @@ __global__ void __launch_bounds__(kNcol * tpc_for<L>()) pass2_kernel(Pass2Args a
   constexpr int kLo = 1 << kP2LoBits;
   constexpr int kHiMax = 512;  // L2*L3 <= 2^17
   // data | stage twiddles | column twiddles W_M^{n3 k1} | W_{L2L3} lo | W_{L2L3} hi
-  __shared__ __attribute__((aligned(16))) float2 smem[Lay::kLds + L + kNcol + kLo + kHiMax];
+  __shared__ __attribute__((aligned(16))) float2 smem[Lay::kLds + kTwPad<L> + kNcol + kLo + kHiMax];
   float2* data = smem;
   float2* twl = smem + Lay::kLds;
-  float2* colw = twl + L;
+  float2* colw = twl + kTwPad<L>;
   float2* lo = colw + kNcol;
   float2* hi = lo + kLo;
 
@@ -137,15 +136,15 @@ __global__ void __launch_bounds__(kNcol * tpc_for<L>()) pass2_kernel(Pass2Args a
   float2* buf = a.buf + static_cast<size_t>(b) * M;
   const size_t base = static_cast<size_t>(k1) * a.L2L3 + n3_0;
 
-  load_stage_twiddles<L>(twl, a.tw);
-  // W_M^{n3 (k1 + L1 k2)} = W_M^{n3 k1} * W_{L2 L3}^{n3 k2};  W_{L2L3}^j = W_2N^{4 L1 j}
-  const uint32_t nhi = (a.L2L3 + kLo - 1) / kLo;
-  for (int i = threadIdx.x; i < kNcol; i += NT) colw[i] = tw_lookup32(a.tw, 4u * (n3_0 + i) * k1);
-  for (int i = threadIdx.x; i < kLo; i += NT) lo[i] = tw_lookup32(a.tw, 4u * a.L1 * static_cast<uint32_t>(i));
-  for (uint32_t i = threadIdx.x; i < nhi; i += NT) hi[i] = tw_lookup32(a.tw, 4u * a.L1 * (i << kP2LoBits));
   int c, tj;
   Lay::coords(threadIdx.x, c, tj);
   for (int r = tj; r < L; r += TPC) data[Lay::idx(r, c)] = buf[base + static_cast<size_t>(r) * a.L3 + c];
+  // W_M^{n3 (k1 + L1 k2)} = W_M^{n3 k1} * W_{L2 L3}^{n3 k2}
+  copy_stage_twiddles<L>(twl, a.tb.st2);
+  const uint32_t nhi = (a.L2L3 + kLo - 1) / kLo;
+  for (int i = threadIdx.x; i < kNcol; i += NT) colw[i] = a.tb.p2col[k1 * a.L3 + n3_0 + i];
+  for (int i = threadIdx.x; i < kLo; i += NT) lo[i] = a.tb.p2lo[i];
+  for (uint32_t i = threadIdx.x; i < nhi; i += NT) hi[i] = a.tb.p2hi[i];
   __syncthreads();
   BlockFFT<L, kNcol, TPC, false>::run(data, twl);
   const uint32_t n3 = n3_0 + c;
@@ -209,18 +208,18 @@ __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Arg
   constexpr int L4 = 4 * L;
   using Lay = BlockLayout<L, NSLOT, TPC, true>;
   // data | stage twiddles W_L | W_{4L} (= W_2N^{C i}) | reduction scratch
-  __shared__ __attribute__((aligned(16))) float2 smem[Lay::kLds + L + L4 + 16];
+  __shared__ __attribute__((aligned(16))) float2 smem[Lay::kLds + kTwPad<L> + L4 + 16];
   float2* data = smem;
   float2* twl = smem + Lay::kLds;
-  float2* t4 = twl + L;
+  float2* t4 = twl + kTwPad<L>;
   double* red = reinterpret_cast<double*>(t4 + L4);
 
   const int b = blockIdx.y;
   const float2* buf = a.buf + static_cast<size_t>(b) * a.M;
-  const uint32_t c0 = blockIdx.x * ROWS;
+  // neighbouring row blocks write neighbouring 32-B pieces of the same output
+  // lines: keep them on one XCD so its L2 merges full lines
+  const uint32_t c0 = xcd_remap(blockIdx.x, gridDim.x) * ROWS;
 
-  load_stage_twiddles<L>(twl, a.tw);
-  for (int i = threadIdx.x; i < L4; i += NT) t4[i] = tw_lookup32(a.tw, a.C * static_cast<uint32_t>(i));
   {
     int slot, tj;
     Lay::coords(threadIdx.x, slot, tj);
@@ -229,6 +228,8 @@ __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Arg
     const float2* src = buf + row_base(row < a.C ? row : 0, a.L1, a.L2, a.L3);
     for (int r = tj; r < L; r += TPC) data[Lay::idx(r, slot)] = src[r];
   }
+  copy_stage_twiddles<L>(twl, a.tb.st3);
+  for (int i = threadIdx.x; i < L4; i += NT) t4[i] = a.tb.p3[i];
   // mean-padding correction delta = (sum of (sample - mu0)) / n_steps
   double delta = 0.0;
   uint32_t n_s = 0;
@@ -240,6 +241,16 @@ __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Arg
     n_s = a.tmpl[b].n_steps;
     delta = tot / static_cast<double>(n_s);
   }
+  // per-row twiddle constants of the untangle phase, fetched before the FFT so
+  // their latency hides under it
+  const int s = threadIdx.x % ROWS;
+  const int t = threadIdx.x / ROWS;
+  constexpr int kStreams = NT / ROWS;
+  const uint32_t c = c0 + s;
+  const uint32_t half = a.C / 2;
+  const uint32_t cm = (a.C - c) % a.C;
+  const RowTw rt = row_twiddles(a.tw, c, n_s);
+  const RowTw rm = row_twiddles(a.tw, cm, n_s);
   __syncthreads();
   BlockFFT<L, NSLOT, TPC, true>::run(data, twl);
 
@@ -267,15 +278,7 @@ __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Arg
   };
 
   // untangle: thread -> (slot s, k3 stream), rows c <= C/2 own their bins
-  const int s = threadIdx.x % ROWS;
-  const int t = threadIdx.x / ROWS;
-  constexpr int kStreams = NT / ROWS;
-  const uint32_t c = c0 + s;
-  const uint32_t half = a.C / 2;
   if (c <= half) {
-    const uint32_t cm = (a.C - c) % a.C;
-    const RowTw rt = row_twiddles(a.tw, c, n_s);
-    const RowTw rm = row_twiddles(a.tw, cm, n_s);
     for (int k3 = t; k3 < L; k3 += kStreams) {
       const float2 zk = data[Lay::idx(k3, s)];
       const int k3m = (c == 0) ? (L - k3) % L : L - 1 - k3;
@@ -312,17 +315,17 @@ __global__ void __launch_bounds__(ROWS * tpc_for<L>()) pass3_plain_kernel(Pass3P
   constexpr int TPC = tpc_for<L>();
   constexpr int NT = ROWS * TPC;
   using Lay = BlockLayout<L, ROWS, TPC, true>;
-  __shared__ __attribute__((aligned(16))) float2 smem[Lay::kLds + L];
+  __shared__ __attribute__((aligned(16))) float2 smem[Lay::kLds + kTwPad<L>];
   float2* data = smem;
   float2* twl = smem + Lay::kLds;
   const uint32_t c0 = blockIdx.x * ROWS;
-  load_stage_twiddles<L>(twl, a.tw);
   {
     int slot, tj;
     Lay::coords(threadIdx.x, slot, tj);
     const float2* src = a.buf + row_base(c0 + slot, a.L1, a.L2, a.L3);
     for (int r = tj; r < L; r += TPC) data[Lay::idx(r, slot)] = src[r];
   }
+  copy_stage_twiddles<L>(twl, a.tb.st3);
   __syncthreads();
   BlockFFT<L, ROWS, TPC, true>::run(data, twl);
   // natural-order output z[c + C*k3] = conj(Z)*scale -> real samples 2n, 2n+1

@@ -25,6 +25,8 @@ namespace {
 constexpr int kThreads = 256;
 constexpr int kHalo = 4;
 constexpr int kSpan = kHsTile + kHalo;
+constexpr int kSpanPad = kSpan + kSpan / 16 + 1;
+__device__ __forceinline__ int sidx(int t) { return t + (t >> 4); }
 
 __device__ __forceinline__ void emit(uint32_t* counter, uint2* list, uint32_t cap, bool pred, uint32_t bin,
                                      float power) {
@@ -44,7 +46,7 @@ __device__ __forceinline__ void emit(uint32_t* counter, uint2* list, uint32_t ca
 
 __global__ void __launch_bounds__(kThreads) harmonic_sum_kernel(HSArgs a) {
 #pragma clang fp contract(off)
-  __shared__ __attribute__((aligned(16))) float sv[4][kSpan];  // S_1..S_4 over the tile + halo
+  __shared__ __attribute__((aligned(16))) float sv[4][kSpanPad];  // S_1..S_4 over the tile + halo
   const int b = blockIdx.y;
   const float* P = a.ps + static_cast<size_t>(b) * a.ps_stride;
   const uint32_t i0 = a.i_start + blockIdx.x * kHsTile;
@@ -65,10 +67,10 @@ __global__ void __launch_bounds__(kThreads) harmonic_sum_kernel(HSArgs a) {
              P[(7u * i + 8u) >> 4] + P[(5u * i + 8u) >> 4] + P[(3u * i + 8u) >> 4] + P[(i + 8u) >> 4];
       s4 = sum;
     }
-    sv[0][t] = s1;
-    sv[1][t] = s2;
-    sv[2][t] = s3;
-    sv[3][t] = s4;
+    sv[0][sidx(t)] = s1;
+    sv[1][sidx(t)] = s2;
+    sv[2][sidx(t)] = s3;
+    sv[3][sidx(t)] = s4;
   }
   __syncthreads();
 
@@ -82,13 +84,14 @@ __global__ void __launch_bounds__(kThreads) harmonic_sum_kernel(HSArgs a) {
     const float p = in ? P[i] : 0.0f;
     emit(&counts[0], cands, a.cap, in && p > thr0, i, p);
   }
-  // levels 1..4: group of 2^h consecutive i starting at s == 2^(h-1) mod 2^h
+  // levels 1..4: group of 2^h consecutive i starting at s == 2^(h-1) mod 2^h;
+  // one thread per group, stride-2^h reads made (nearly) conflict free by the
+  // t + t/16 padding of sv
 #pragma unroll
   for (int h = 1; h <= 4; ++h) {
     const int g = 1 << h;
     const int off = g >> 1;
     const float thr = a.thr[h];
-    // first group start >= i0 with start == off (mod g); i0 == 8 (mod 16)
     const int first = static_cast<int>((off - (i0 % g) + g) % g);
     const int ngroups = (kHsTile - first + g - 1) / g;
     for (int q = threadIdx.x; q < ((ngroups + kThreads - 1) / kThreads) * kThreads; q += kThreads) {
@@ -97,10 +100,11 @@ __global__ void __launch_bounds__(kThreads) harmonic_sum_kernel(HSArgs a) {
       float m = ninf;
       if (q < ngroups) {
         const int t0 = first + q * g;
-        const uint32_t s = i0 + t0;
-        j = (s + off) >> h;
+        j = (i0 + static_cast<uint32_t>(t0) + off) >> h;
         if (j >= a.w2 && j < a.fhi) {
-          for (int u = 0; u < g; ++u) m = fmaxf(m, sv[h - 1][t0 + u]);
+#pragma unroll
+          for (int u = 0; u < 16; ++u)
+            if (u < g) m = fmaxf(m, sv[h - 1][sidx(t0 + u)]);
           pred = m > thr;
         }
       }

@@ -58,6 +58,16 @@ __device__ __forceinline__ float2 tw_lookup32(const TwiddleTable& t, uint32_t j)
   return cmul(a, b);
 }
 
+// XCD-aware workgroup order: the dispatcher deals workgroups round-robin over
+// the 8 XCDs (b, b+8, ... share one XCD and its L2). Remap so that each XCD
+// gets a contiguous range of logical workgroups (bijective for any nwg).
+// Placement is a speed hint only; correctness never depends on it.
+__device__ __forceinline__ uint32_t xcd_remap(uint32_t bid, uint32_t nwg) {
+  constexpr uint32_t kXcd = 8;
+  const uint32_t q = nwg / kXcd, r = nwg % kXcd, x = bid % kXcd, k = bid / kXcd;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
+}
+
 // wave-level sum (64 lanes) of a double
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
