@@ -56,7 +56,9 @@ def resample(series: np.ndarray, geom: dict, P: float, tau: float, psi0: float):
     idx = (np.float32(i[:n_steps] - del_t[:n_steps]).astype(np.float64) + 0.5).astype(np.int64)
     out = np.empty(n, np.float32)
     out[:n_steps] = series[np.clip(idx, 0, nu - 1)]
-    mean = np.float32(np.sum(out[:n_steps], dtype=np.float64) / n_steps)
+    # sequential float accumulation, divided by the float sample count
+    # (demod_binary_resamp_cpu.c:112-125); cumsum is sequential, sum is pairwise
+    mean = np.float32(np.cumsum(out[:n_steps], dtype=np.float32)[-1] / np.float32(n_steps))
     out[n_steps:] = mean
     return out, n_steps, mean
 
@@ -68,8 +70,13 @@ def power_spectrum(x: np.ndarray, fft_size: int) -> np.ndarray:
     return ps
 
 
-def harmonic_sums(ps: np.ndarray, geom: dict) -> np.ndarray:
-    """sumspec[h][j] for h=0..4, j < fundamental_idx_hi (max over i, reference float order)."""
+def harmonic_sums(ps: np.ndarray, geom: dict, thr=None) -> np.ndarray:
+    """sumspec[h][j] for h=0..4, j < fundamental_idx_hi (reference float order).
+
+    Without `thr`: the max of S_h(i) over the cell's i. With `thr`: the
+    reference's exact array contents (hs_common.c:78-165) -- a cell is
+    rewritten only on its first visit or when the running max exceeds thr[h],
+    so cells whose max stays <= thr[h] keep the first visited S_h(i)."""
     w2, fhi, hhi = int(geom["window_2"]), int(geom["fundamental_idx_hi"]), int(geom["harmonic_idx_hi"])
     i = np.arange(w2, hhi, dtype=np.int64)
     P = ps.astype(np.float32)
@@ -95,6 +102,10 @@ def harmonic_sums(ps: np.ndarray, geom: dict) -> np.ndarray:
         j = (i + (1 << (h - 1))) >> h
         m = j < fhi
         np.maximum.at(out[h], j[m], S[m])
+        if thr is not None:
+            jj, first = np.unique(j[m], return_index=True)
+            low = out[h][jj] <= np.float32(thr[h])
+            out[h][jj[low]] = np.maximum(S[m][first[low]], np.float32(0.0))
     return out
 
 

@@ -1,0 +1,169 @@
+"""End-to-end searches on the CPU golden backend: the Python driver, the BOINC
+application binary (wrapper + MAIN parser), checkpoint/resume under fault
+injection, and the command-line contract (erp_boinc_wrapper.cpp:147-300,
+demod_binary.c:117-700)."""
+import os
+import subprocess
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from boinc_app_eah_brp_amd.models import BRPSearch, SearchConfig
+from boinc_app_eah_brp_amd.models.search import app_binary
+from boinc_app_eah_brp_amd.utils import synth
+
+INJ = synth.Injection(f0=211.0, P_orb=900.0, tau=0.03, psi0=0.7, amplitude=3.0)
+
+
+@pytest.fixture(scope="module")
+def case(tmp_path_factory):
+    d = tmp_path_factory.mktemp("case")
+    return synth.synthetic_case(d, n=1 << 15, n_templates=23, inj=INJ)
+
+
+@pytest.fixture(scope="module")
+def app(brp):
+    p = app_binary()
+    if not p.exists():
+        from boinc_app_eah_brp_amd import _build
+
+        _build.build()
+    assert p.exists()
+    return p
+
+
+def _cfg(case, d, **kw):
+    d = Path(d)
+    return SearchConfig(inputfile=case["wu"], templatebank=case["bank"], zaplistfile=case["zap"],
+                        outputfile=str(d / "out.cand"), checkpointfile=str(d / "cp.cpt"), f0=400.0, padding=3.0,
+                        fA=0.08, window=100, white=True, batch=4, use_cpu=True, **kw)
+
+
+def _result_lines(path):
+    return [l for l in Path(path).read_text().splitlines() if l and not l.startswith("%") or l == "%DONE%"]
+
+
+def test_cpu_search_finds_injection(brp, case, tmp_path):
+    s = BRPSearch(_cfg(case, tmp_path))
+    out = s.run()
+    assert out.templates_run == out.templates_total == 24
+    lines, done = s.results()
+    assert done and lines
+    f, P, tau, psi, power, fa, nh = lines[0]
+    # the strongest candidate is the injected spin frequency (or a harmonic of it)
+    r = f / INJ.f0
+    assert abs(r - round(r)) < 0.01 or abs(1 / r - round(1 / r)) < 0.01, lines[:3]
+    assert fa > 20
+
+
+def test_python_driver_block_runs_merge_to_full(brp, case, tmp_path):
+    full = BRPSearch(_cfg(case, tmp_path / "a")).run(write_output=False, use_checkpoint=False)
+    tables = []
+    for b, e in ((0, 7), (7, 8), (8, 24)):
+        o = BRPSearch(_cfg(case, tmp_path / "b")).run(begin=b, end=e, write_output=False, use_checkpoint=False)
+        tables.append(o.table)
+    merged = brp.CandidateTable()
+    for t in tables:
+        merged.merge(t)
+    assert bytes(full.table.to_bytes()) == bytes(merged.to_bytes())
+
+
+def _app_args(case, d, extra=()):
+    d = Path(d)
+    return ["-i", case["wu"], "-t", case["bank"], "-l", case["zap"], "-o", str(d / "res.cand"), "-c",
+            str(d / "cp.cpt"), "-A", "0.08", "-P", "3.0", "-f", "400.0", "-W", "-B", "100", "--mi355x-cpu", *extra]
+
+
+def _run_app(app, args, cwd, **env):
+    e = dict(os.environ, BRP_NO_RESULT_HEADER="1", **env)
+    return subprocess.run([str(app), *args], cwd=cwd, env=e, capture_output=True, text=True, timeout=300)
+
+
+def test_app_checkpoint_resume_after_fault(app, case, tmp_path):
+    ref_dir, run_dir = tmp_path / "ref", tmp_path / "run"
+    ref_dir.mkdir()
+    run_dir.mkdir()
+    r = _run_app(app, _app_args(case, ref_dir), ref_dir)
+    assert r.returncode == 0, r.stderr[-2000:]
+    ref = _result_lines(ref_dir / "res.cand")
+    assert ref[-1] == "%DONE%"
+    # checkpoint file is removed after a successful pass
+    assert not (ref_dir / "cp.cpt").exists()
+
+    # interrupted after 9 templates (checkpoint every template), then resumed
+    r = _run_app(app, _app_args(case, run_dir), run_dir, BRP_FAULT="kill_after_template:9", BRP_CHECKPOINT_PERIOD="0")
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert not (run_dir / "res.cand").exists()
+    assert (run_dir / "cp.cpt").exists()
+    import boinc_app_eah_brp_amd as pkg
+
+    n, orig, _ = pkg.native().read_checkpoint(str(run_dir / "cp.cpt"))
+    assert 9 <= n < 24 and orig == case["wu"]
+    r = _run_app(app, _app_args(case, run_dir), run_dir)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "Continuing work on" in r.stderr or "checkpoint" in r.stderr.lower()
+    assert _result_lines(run_dir / "res.cand") == ref
+
+
+def test_app_skips_existing_output(app, case, tmp_path):
+    (tmp_path / "res.cand").write_text("keep\n")
+    r = _run_app(app, _app_args(case, tmp_path), tmp_path)
+    assert r.returncode == 0
+    assert "already exists" in r.stderr
+    assert (tmp_path / "res.cand").read_text() == "keep\n"
+
+
+def test_app_rejects_checkpoint_of_other_input(app, brp, case, tmp_path):
+    brp.write_checkpoint(str(tmp_path / "cp.cpt"), 3, "some_other_file.bin4", brp.CandidateTable())
+    r = _run_app(app, _app_args(case, tmp_path), tmp_path)
+    assert r.returncode != 0
+    assert "doesn't agree" in r.stderr
+
+
+def test_app_option_errors(app, case, tmp_path):
+    # -K (kill line) is accepted by the wrapper but rejected by MAIN (reference quirk)
+    r = _run_app(app, _app_args(case, tmp_path, ["-K"]), tmp_path)
+    assert r.returncode != 0
+    # unequal numbers of -i and -o
+    r = _run_app(app, ["-i", case["wu"], "-t", case["bank"]], tmp_path)
+    assert r.returncode != 0
+    r = _run_app(app, ["--version"], tmp_path)
+    assert r.returncode == 0 and "Binary Pulsar Search Revision" in r.stderr + r.stdout
+
+
+def test_app_soft_link_resolution(app, case, tmp_path):
+    # BOINC logical names: a file containing <soft_link>physical</soft_link>
+    (tmp_path / "logical_wu").write_text(f"<soft_link>{case['wu']}</soft_link>\n")
+    args = _app_args(case, tmp_path)
+    args[1] = "logical_wu"
+    # the checkpoint header holds the physical file name
+    r = _run_app(app, args, tmp_path, BRP_FAULT="kill_after_template:2", BRP_CHECKPOINT_PERIOD="0")
+    assert r.returncode == 0, r.stderr[-2000:]
+    import boinc_app_eah_brp_amd as pkg
+
+    _, orig, _ = pkg.native().read_checkpoint(str(tmp_path / "cp.cpt"))
+    assert orig == case["wu"]
+
+
+def test_search_main_in_process(brp, case, tmp_path):
+    rc = BRPSearch.command_line(["prog", *_app_args(case, tmp_path)])
+    assert rc == 0
+    lines, done = brp.read_results(str(tmp_path / "res.cand"))
+    assert done and len(lines) > 0
+    # invalid option value
+    assert BRPSearch.command_line(["prog", "-P", "0.5", *_app_args(case, tmp_path)[0:4]]) != 0
+
+
+def test_shmem_xml_render(brp):
+    xml = brp.render_shmem_xml()
+    # element names of erp_boinc_ipc.cpp:84-160
+    for tag in ("<graphics_info>", "<skypos_rac>", "<skypos_dec>", "<dispersion>", "<orb_radius>", "<orb_period>",
+                "<orb_phase>", "<power_spectrum>", "<fraction_done>", "<cpu_time>", "<update_time>",
+                "<boinc_status>", "<quit_request>", "<max_working_set_size>"):
+        assert tag in xml, tag
+    # 40-bin screensaver spectrum as two zero-padded hex digits per bin
+    import re
+
+    m = re.search(r"<power_spectrum>([0-9a-f]*)</power_spectrum>", xml)
+    assert m is not None and len(m.group(1)) == 80
