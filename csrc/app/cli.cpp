@@ -39,7 +39,7 @@ void print_usage(const char* prog) {
   std::printf(" -D, --device\t\tinteger\tThe GPU device ID to be used.\n");
   std::printf(" -z, --debug\t\t\tboolean\tRun program in debug mode.\n");
   std::printf(" --mi355x-batch\t\tinteger\tTemplates per device batch (default 4).\n");
-  std::printf(" --mi355x-gpus\t\tinteger\tNumber of GPUs driven by this process (default 1).\n");
+  std::printf(" --mi355x-gpus\t\tinteger\tGPUs (or CPU worker threads with --mi355x-cpu) driven by this process (default 1).\n");
   std::printf(" --mi355x-cpu\t\t\tboolean\tUse the CPU golden backend.\n");
   std::printf("\n");
 }

@@ -197,11 +197,22 @@ int SearchSession::open(const SearchOptions& opt, const SearchControl& ctl) {
     for (int h = 0; h < 5; ++h)
       log_message(LOG_INFO, false, "%s = %g\n", names[h], 0.5 * chisq_Qinv_even(d.g.prob, 1 << h));
   }
-  const int ngpu = opt.use_cpu ? 1 : std::max(1, ctl.gpus);
+  // one backend per device; with the CPU golden model, one per worker thread
+  int ngpu = std::max(1, ctl.gpus);
+  if (!d.opt.use_cpu && !hip_backend_supports(d.g)) {
+    // FFTW accepts any length; the HIP FFT is compiled for N/2 = L1*L2*L3 over
+    // 16*2^a*3^b*5^c lengths. Other paddings run on the CPU golden model.
+    const int nt = std::max(1, std::min(64, static_cast<int>(std::thread::hardware_concurrency())));
+    log_message(LOG_WARN, true,
+                "No HIP FFT plan for N = %u (padding %.3f): using the CPU backend with %d threads.\n", d.g.nsamples,
+                d.opt.padding, nt);
+    d.opt.use_cpu = true;
+    ngpu = nt;
+  }
   boinc::begin_critical_section();
   for (int k = 0; k < ngpu; ++k) {
     std::unique_ptr<Backend> b;
-    if (opt.use_cpu) {
+    if (d.opt.use_cpu) {
       b = make_cpu_backend();
     } else {
       int dev = opt.device;
@@ -226,6 +237,7 @@ int SearchSession::prepare() {
   if (rc) return rc;
   SearchOptions opt_nw = d.opt;
   opt_nw.white = false;
+  opt_nw.prewhitened = d.opt.white;
   for (size_t k = 1; k < d.backends.size(); ++k) {
     std::vector<float> s = d.series;
     rc = d.backends[k]->setup(d.g, opt_nw, s, d.zaps);

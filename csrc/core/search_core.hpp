@@ -23,6 +23,7 @@ struct SearchOptions {
   // MI355X extensions (not part of the BOINC command line)
   int batch = 0;            // templates per device batch (0 = auto)
   bool use_cpu = false;     // CPU golden backend instead of HIP
+  bool prewhitened = false; // series already whitened by another backend (DC removed)
 };
 
 // Everything derived from the WU header + options (demod_binary.c:778-782,

@@ -48,6 +48,9 @@ class Backend {
 
 std::unique_ptr<Backend> make_cpu_backend();
 // device < 0: auto (BOINC gpu_device_num / first device)
+// True when the HIP pipeline has a compiled FFT plan for this geometry
+// (N even and N/2 = L1*L2*L3 over the compiled lengths, fft_passes.hip).
+bool hip_backend_supports(const SearchGeometry& g);
 std::unique_ptr<Backend> make_hip_backend(int device, int batch, int* err);
 
 }  // namespace brp

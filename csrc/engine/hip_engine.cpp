@@ -34,8 +34,9 @@ using hipk::TemplateDev;
 
 bool make_fft_plan(uint32_t M, FFTPlan3& plan) {
   plan = FFTPlan3();
-  static const uint32_t p3[] = {256, 128, 64};
-  static const uint32_t p12[] = {512, 384, 256, 192, 128, 96, 64, 48, 32, 16};
+  // preference: long pass-3 rows (contiguous PS writes), then balanced L1 >= L2
+  static const uint32_t p3[] = {256, 320, 192, 160, 128, 96, 64};
+  static const uint32_t p12[] = {512, 384, 320, 288, 256, 240, 192, 160, 144, 128, 96, 80, 64, 48, 32, 16};
   for (uint32_t L3 : p3) {
     if (M % L3) continue;
     const uint32_t R = M / L3;
@@ -693,12 +694,19 @@ int HipEngine::benchmark_stages(const TemplateInput* t, int n, int reps, std::ve
   BRP_HIP_CHECK(hipStreamSynchronize(d.stream), RADPUL_HIP_KERNEL_INVOKE);
   us_per_launch.assign(Impl::kNumStages + 1, 0.0);
   for (int st = 0; st <= Impl::kNumStages; ++st) {
-    // st == kNumStages: the whole pipeline
+    // st == kNumStages: the whole pipeline. Every stage starts from the data of
+    // one full run (pass 2 works in place, so repeating it alone drifts the data).
+    BRP_HIP_CHECK(d.enqueue(nb), RADPUL_HIP_KERNEL_INVOKE);
     BRP_HIP_CHECK(hipEventRecord(d.ev0, d.stream), RADPUL_HIP_KERNEL_INVOKE);
     for (int r = 0; r < reps; ++r) {
       if (st == Impl::kNumStages) {
         BRP_HIP_CHECK(d.enqueue(nb), RADPUL_HIP_KERNEL_INVOKE);
       } else {
+        // the harmonic stage appends to the candidate lists: reset their
+        // counters (a 100-byte memset) so every repetition sees the same load
+        if (st == Impl::kHarmonic)
+          BRP_HIP_CHECK(hipMemsetAsync(d.counts.p, 0, sizeof(uint32_t) * kNumHarmonicLevels * nb, d.stream),
+                        RADPUL_HIP_KERNEL_INVOKE);
         BRP_HIP_CHECK(d.enqueue_stage(st, nb), RADPUL_HIP_KERNEL_INVOKE);
       }
     }
@@ -724,9 +732,14 @@ class HipBackend final : public Backend {
   int init(int device, int batch) { return eng_.init(device, batch); }
   int setup(const SearchGeometry& g, const SearchOptions& opt, std::vector<float>& series,
             const std::vector<ZapRange>& zaps) override {
+    // padding offset mu0 (the padded FFT is corrected to the reference's mean
+    // padding by linearity); a whitened series has its DC removed: mu0 = 0, the
+    // value the whitening backend itself uses, so all devices compute identical spectra
     double mean = 0.0;
-    for (float v : series) mean += v;
-    mean = series.empty() ? 0.0 : mean / series.size();
+    if (!opt.prewhitened) {
+      for (float v : series) mean += v;
+      mean = series.empty() ? 0.0 : mean / series.size();
+    }
     int rc = eng_.setup(g, series, static_cast<float>(mean));
     if (rc) return rc;
     if (opt.white) return eng_.whiten(opt, zaps, series);
@@ -743,6 +756,11 @@ class HipBackend final : public Backend {
   HipEngine eng_;
 };
 }  // namespace
+
+bool hip_backend_supports(const SearchGeometry& g) {
+  FFTPlan3 p;
+  return g.nsamples % 2 == 0 && make_fft_plan(g.nsamples / 2, p);
+}
 
 std::unique_ptr<Backend> make_hip_backend(int device, int batch, int* err) {
   auto b = std::make_unique<HipBackend>();

@@ -240,9 +240,11 @@ template <> struct Radices<64> { template <template <int...> class F> using appl
 template <> struct Radices<80> { template <template <int...> class F> using apply = F<5, 16>; };
 template <> struct Radices<96> { template <template <int...> class F> using apply = F<3, 2, 16>; };
 template <> struct Radices<128> { template <template <int...> class F> using apply = F<8, 16>; };
+template <> struct Radices<144> { template <template <int...> class F> using apply = F<3, 3, 16>; };
 template <> struct Radices<160> { template <template <int...> class F> using apply = F<5, 2, 16>; };
 template <> struct Radices<192> { template <template <int...> class F> using apply = F<3, 4, 16>; };
 template <> struct Radices<240> { template <template <int...> class F> using apply = F<3, 5, 16>; };
+template <> struct Radices<288> { template <template <int...> class F> using apply = F<3, 3, 2, 16>; };
 template <> struct Radices<256> { template <template <int...> class F> using apply = F<16, 16>; };
 template <> struct Radices<320> { template <template <int...> class F> using apply = F<5, 4, 16>; };
 template <> struct Radices<384> { template <template <int...> class F> using apply = F<3, 8, 16>; };

@@ -344,8 +344,11 @@ __global__ void __launch_bounds__(ROWS * tpc_for<L>()) pass3_plain_kernel(Pass3P
 }  // namespace
 
 // ------------------------------------------------------------ dispatch glue
-#define BRP_P12_LENGTHS(X) X(16) X(32) X(48) X(64) X(96) X(128) X(192) X(256) X(384) X(512)
-#define BRP_P3_LENGTHS(X) X(64) X(128) X(256)
+// Compiled lengths (any 16 * 2^a 3^b 5^c with a radix list in fft_block.hpp
+// can be added): N/2 = L1 * L2 * L3 must factor over these sets.
+#define BRP_P12_LENGTHS(X) \
+  X(16) X(32) X(48) X(64) X(80) X(96) X(128) X(144) X(160) X(192) X(240) X(256) X(288) X(320) X(384) X(512)
+#define BRP_P3_LENGTHS(X) X(64) X(96) X(128) X(160) X(192) X(256) X(320)
 
 bool pass12_length_supported(uint32_t L) {
   switch (L) {

@@ -35,9 +35,11 @@ def app(brp):
 
 def _cfg(case, d, **kw):
     d = Path(d)
-    return SearchConfig(inputfile=case["wu"], templatebank=case["bank"], zaplistfile=case["zap"],
-                        outputfile=str(d / "out.cand"), checkpointfile=str(d / "cp.cpt"), f0=400.0, padding=3.0,
-                        fA=0.08, window=100, white=True, batch=4, use_cpu=True, **kw)
+    base = dict(inputfile=case["wu"], templatebank=case["bank"], zaplistfile=case["zap"],
+                outputfile=str(d / "out.cand"), checkpointfile=str(d / "cp.cpt"), f0=400.0, padding=3.0, fA=0.08,
+                window=100, white=True, batch=4, use_cpu=True)
+    base.update(kw)
+    return SearchConfig(**base)
 
 
 def _result_lines(path):
@@ -167,3 +169,13 @@ def test_shmem_xml_render(brp):
 
     m = re.search(r"<power_spectrum>([0-9a-f]*)</power_spectrum>", xml)
     assert m is not None and len(m.group(1)) == 80
+
+
+def test_unsupported_fft_length_falls_back_to_cpu(brp, case, tmp_path):
+    # padding 1.3 -> N/2 has a prime factor the HIP FFT is not compiled for:
+    # the session switches to the CPU golden model (with a warning) instead of failing
+    cfg = _cfg(case, tmp_path, padding=1.3, use_cpu=False)
+    out = BRPSearch(cfg).run(end=3, write_output=False, use_checkpoint=False)
+    assert out.templates_run == 3
+    M = out.geometry["nsamples"] // 2
+    assert brp.fft_plan(M) is None

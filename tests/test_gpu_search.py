@@ -1,0 +1,137 @@
+"""End-to-end searches on the MI355X against the CPU golden model
+(pytest -m gpu). The HIP path must be the one that runs: HipEngine raises if
+the device or the extension is missing, there is no silent fallback."""
+import os
+import subprocess
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from boinc_app_eah_brp_amd.models import BRPSearch, SearchConfig
+from boinc_app_eah_brp_amd.models.search import app_binary
+from boinc_app_eah_brp_amd.utils import synth
+
+from conftest import BANK, WU, ZAP
+
+pytestmark = pytest.mark.gpu
+
+INJ = synth.Injection(f0=211.0, P_orb=900.0, tau=0.03, psi0=0.7, amplitude=3.0)
+
+
+@pytest.fixture(scope="module")
+def case(tmp_path_factory):
+    return synth.synthetic_case(tmp_path_factory.mktemp("gcase"), n=1 << 16, n_templates=37, inj=INJ)
+
+
+def _cfg(case, d, **kw):
+    d = Path(d)
+    d.mkdir(parents=True, exist_ok=True)
+    base = dict(inputfile=case["wu"], templatebank=case["bank"], zaplistfile=case["zap"],
+                outputfile=str(d / "out.cand"), checkpointfile=str(d / "cp.cpt"), f0=400.0, padding=3.0, fA=0.08,
+                window=100, white=True, batch=4)
+    base.update(kw)
+    return SearchConfig(**base)
+
+
+def _entries(table):
+    return [e for e in table.entries() if e[5] > 0]
+
+
+def _compare_tables(t_gpu, t_cpu, rtol=2e-4):
+    """Same candidate bins per level; powers within float-FFT tolerance."""
+    eg, ec = t_gpu.entries(), t_cpu.entries()
+    for h in range(5):
+        g = {e[0]: e for e in eg[h * 100:(h + 1) * 100] if e[5] > 0}
+        c = {e[0]: e for e in ec[h * 100:(h + 1) * 100] if e[5] > 0}
+        # entries at the bottom of a full level may differ by near-ties; require
+        # the strongest 90% to agree exactly in bin
+        strong = sorted(c.values(), key=lambda e: -e[1])[:max(1, int(0.9 * len(c)))]
+        for e in strong:
+            assert e[0] in g, (h, e)
+            assert g[e[0]][1] == pytest.approx(e[1], rel=rtol), (h, e, g[e[0]])
+        assert abs(len(g) - len(c)) <= max(1, len(c) // 10)
+
+
+@pytest.mark.parametrize("n,padding", [(1 << 15, 1.0), (1 << 16, 2.0), (3 << 14, 3.0), (5 << 14, 1.0)])
+def test_fft_plans_power_spectrum(brp, gpu, tmp_path, n, padding):
+    """Different FFT factorisations (L1 x L2 x L3) against the double CPU FFT."""
+    x = synth.make_series(n, 65.476, synth.Injection(f0=97.0, P_orb=700.0, tau=0.02, psi0=0.3, amplitude=2.0))
+    wu = synth.write_wu(tmp_path / "a.bin4", x)
+    hdr, series, _ = brp.read_work_unit(str(wu))
+    geom = brp.derive_geometry(hdr, dict(f0=150.0, padding=padding, fA=0.08, window=100))
+    M = geom["nsamples"] // 2
+    assert brp.fft_plan(M) is not None, M
+    eng = brp.HipEngine()
+    eng.init(0, 2)
+    eng.setup(geom, series, float(np.mean(series)))
+    for P, tau, psi in ((700.0, 0.02, 0.3), (1500.0, 0.3, 4.0)):
+        ps_g, ns_g = eng.power_spectrum(P, tau, psi)
+        xr, ns_c, _ = brp.cpu_resample(series, geom, P, tau, psi)
+        ps_c = brp.cpu_power_spectrum(xr, geom["fft_size"])
+        assert ns_g == ns_c
+        scale = float(np.mean(ps_c[1:]))
+        err = np.abs(ps_g.astype(np.float64) - ps_c)[1:] / np.maximum(ps_c[1:], scale)
+        assert err.max() < 2e-4, (n, padding, err.max())
+
+
+def test_gpu_search_matches_cpu(brp, gpu, case, tmp_path):
+    g = BRPSearch(_cfg(case, tmp_path / "g")).run()
+    c = BRPSearch(_cfg(case, tmp_path / "c", use_cpu=True)).run()
+    assert g.templates_run == c.templates_run == 38
+    _compare_tables(g.table, c.table)
+    lg, _ = brp.read_results(str(tmp_path / "g" / "out.cand"))
+    lc, _ = brp.read_results(str(tmp_path / "c" / "out.cand"))
+    # the top result lines (strongest candidates) agree
+    for a, b in zip(lg[:10], lc[:10]):
+        assert a[0] == pytest.approx(b[0], rel=1e-9) and a[6] == b[6]
+        assert a[4] == pytest.approx(b[4], rel=2e-4)
+
+
+def test_gpu_block_runs_merge_to_full(brp, gpu, case, tmp_path):
+    full = BRPSearch(_cfg(case, tmp_path / "f")).run(write_output=False, use_checkpoint=False)
+    merged = brp.CandidateTable()
+    for b, e in ((0, 9), (9, 10), (10, 38)):
+        o = BRPSearch(_cfg(case, tmp_path / "p", batch=3)).run(begin=b, end=e, write_output=False,
+                                                               use_checkpoint=False)
+        merged.merge(o.table)
+    _compare_tables(merged, full.table, rtol=1e-6)
+
+
+def test_two_backends_one_process(brp, gpu, case, tmp_path):
+    """Two device backends fed by worker threads, applied in template order
+    (the in-process multi-GPU path; both on device 0 on a one-GPU box)."""
+    opts = _cfg(case, tmp_path / "m").options()
+    s = brp.SearchSession()
+    s.open(opts, 2, [0, 0])
+    s.prepare()
+    t2, _ = s.run(0, s.total(), brp.CandidateTable())
+    one = BRPSearch(_cfg(case, tmp_path / "o")).run(write_output=False, use_checkpoint=False)
+    assert bytes(t2.to_bytes()) == bytes(one.table.to_bytes())
+
+
+def test_bench_wu_prefix_vs_cpu_golden(brp, gpu, tmp_path):
+    """First templates of the benchmark WU (whitened, 3*2^22-point FFT) on the GPU
+    vs the CPU golden model."""
+    kw = dict(batch=4)
+    cfg = SearchConfig.benchmark(str(WU), str(BANK), str(ZAP), outputfile=str(tmp_path / "g.cand"), **kw)
+    g = BRPSearch(cfg).run(begin=0, end=12, write_output=False, use_checkpoint=False)
+    cfgc = SearchConfig.benchmark(str(WU), str(BANK), str(ZAP), outputfile=str(tmp_path / "c.cand"), batch=1,
+                                  use_cpu=True)
+    c = BRPSearch(cfgc, gpus=12).run(begin=0, end=12, write_output=False, use_checkpoint=False)
+    _compare_tables(g.table, c.table)
+
+
+def test_app_binary_gpu(brp, gpu, case, tmp_path):
+    app = app_binary()
+    assert app.exists()
+    args = ["-i", case["wu"], "-t", case["bank"], "-l", case["zap"], "-o", str(tmp_path / "res.cand"), "-c",
+            str(tmp_path / "cp.cpt"), "-A", "0.08", "-P", "3.0", "-f", "400.0", "-W", "-B", "100"]
+    env = dict(os.environ, BRP_NO_RESULT_HEADER="1")
+    r = subprocess.run([str(app), *args], cwd=tmp_path, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines, done = brp.read_results(str(tmp_path / "res.cand"))
+    assert done and lines
+    rc = BRPSearch(_cfg(case, tmp_path / "c", use_cpu=True)).run()
+    lc, _ = brp.read_results(str(tmp_path / "c" / "out.cand"))
+    assert lines[0][0] == pytest.approx(lc[0][0], rel=1e-9)
