@@ -154,6 +154,7 @@ struct HipEngine::Impl {
   FFTPlan3 plan;
   bool ready = false;
   float mu0 = 0.0f;
+  uint32_t p3_exp = 0;          // BRP_P3_EXP profiling switches (pass3_kernel)
   uint32_t ps_stride = 0;
   uint32_t i_start = 0;
 
@@ -161,6 +162,7 @@ struct HipEngine::Impl {
   DevBuf<float2> buf;           // [batch][M]
   DevBuf<float> ps;             // [batch][ps_stride]
   DevBuf<double> partials;      // [batch][wg1]
+  DevBuf<double> delta;         // [batch] mean-padding correction
   DevBuf<TemplateDev> tmpl;     // [batch]
   DevBuf<float> thr;            // [5]
   DevBuf<uint32_t> counts;      // [batch][5]
@@ -275,6 +277,10 @@ struct HipEngine::Impl {
         a2.L3 = plan.L3;
         a2.tw = tw;
         a2.tb = tables();
+        a2.partials = partials.p;
+        a2.n_partials = plan.wg1();
+        a2.tmpl = tmpl.p;
+        a2.delta = delta.p;
         return hipk::launch_pass2(plan, a2, nb, stream);
       }
       case kPass3: {
@@ -288,12 +294,12 @@ struct HipEngine::Impl {
         a3.tw = tw;
         a3.tb = tables();
         a3.limit = std::min(g.harmonic_idx_hi, g.fft_size);
+        a3.exp = p3_exp;
         a3.ps = ps.p;
         a3.ps_stride = ps_stride;
         a3.norm = static_cast<float>(1.0 / g.nsamples);
         a3.tmpl = tmpl.p;
-        a3.partials = partials.p;
-        a3.n_partials = plan.wg1();
+        a3.delta = delta.p;
         return hipk::launch_pass3(plan, hipk::P3_POWER, a3, nb, stream);
       }
       case kHarmonic: {
@@ -343,6 +349,7 @@ int HipEngine::init(int device, int batch) {
     log_message(LOG_ERROR, true, "No HIP device available.\n");
     return RADPUL_HIP_DEVICE_FIND;
   }
+  if (const char* e = std::getenv("BRP_P3_EXP")) impl_->p3_exp = static_cast<uint32_t>(std::atoi(e));
   if (device < 0) {
     const char* env = std::getenv("BRP_DEVICE");
     device = env ? std::atoi(env) : 0;
@@ -388,6 +395,7 @@ int HipEngine::setup(const SearchGeometry& g, const std::vector<float>& series, 
   if ((rc = d.buf.alloc(B * d.plan.M))) return rc;
   if ((rc = d.ps.alloc(B * d.ps_stride))) return rc;
   if ((rc = d.partials.alloc(B * d.plan.wg1()))) return rc;
+  if ((rc = d.delta.alloc(B))) return rc;
   if ((rc = d.tmpl.alloc(B))) return rc;
   if ((rc = d.thr.alloc(kNumHarmonicLevels))) return rc;
   if ((rc = d.counts.alloc(B * kNumHarmonicLevels))) return rc;
@@ -647,6 +655,10 @@ int HipEngine::power_spectrum(const TemplateInput& t, std::vector<float>& ps_out
   a2.L3 = d.plan.L3;
   a2.tw = tw;
   a2.tb = d.tables();
+  a2.partials = d.partials.p;
+  a2.n_partials = d.plan.wg1();
+  a2.tmpl = d.tmpl.p;
+  a2.delta = d.delta.p;
   BRP_HIP_CHECK(hipk::launch_pass2(d.plan, a2, 1, s), RADPUL_HIP_KERNEL_INVOKE);
   DevBuf<float> full;
   int rc;
@@ -665,8 +677,7 @@ int HipEngine::power_spectrum(const TemplateInput& t, std::vector<float>& ps_out
   a3.ps_stride = g.fft_size;
   a3.norm = static_cast<float>(1.0 / g.nsamples);
   a3.tmpl = d.tmpl.p;
-  a3.partials = d.partials.p;
-  a3.n_partials = d.plan.wg1();
+  a3.delta = d.delta.p;
   BRP_HIP_CHECK(hipk::launch_pass3(d.plan, hipk::P3_POWER, a3, 1, s), RADPUL_HIP_KERNEL_INVOKE);
   ps_out.resize(g.fft_size);
   BRP_HIP_CHECK(hipMemcpyAsync(ps_out.data(), full.p, g.fft_size * sizeof(float), hipMemcpyDeviceToHost, s),

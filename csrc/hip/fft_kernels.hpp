@@ -63,6 +63,13 @@ struct Pass2Args {
   uint32_t L1, L2L3, L3;
   TwiddleTable tw;
   FFTTables tb;
+  // mean-padding correction (template pipeline only, else nullptr): workgroup 0
+  // of each template reduces pass 1's partial sums once, in a fixed order,
+  // delta[b] = sum / n_steps
+  const double* partials;      // [batch][n_partials]
+  uint32_t n_partials;
+  const TemplateDev* tmpl;
+  double* delta;               // [batch]
 };
 
 enum Pass3Mode : int {
@@ -82,10 +89,10 @@ struct Pass3Args {
   uint32_t ps_stride;
   float norm;                  // 1/N (float)
   const TemplateDev* tmpl;     // n_steps per template
-  const double* partials;      // [batch][n_partials]
-  uint32_t n_partials;
+  const double* delta;         // [batch] mean-padding correction (pass 2)
   // P3_COMPLEX
   float2* spec;                // fft_size complex bins
+  uint32_t exp;                // profiling experiments (BRP_P3_EXP), 0 in production
 };
 
 // plain row pass of the inverse transform: conj, scale, write the first

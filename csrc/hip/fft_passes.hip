@@ -154,6 +154,17 @@ __global__ void __launch_bounds__(kNcol * tpc_for<L>()) pass2_kernel(Pass2Args a
     const float2 w = cmul(wc, cmul(hi[e >> kP2LoBits], lo[e & (kLo - 1)]));
     buf[base + static_cast<size_t>(k2) * a.L3 + c] = cmul(data[Lay::idx(k2, c)], w);
   }
+  if (a.partials != nullptr && blockIdx.x == 0) {
+    __shared__ double red[NT / kWave + 1];
+    const double* pp = a.partials + static_cast<size_t>(b) * a.n_partials;
+    double part = 0.0;
+    for (uint32_t i = threadIdx.x; i < a.n_partials; i += NT) part += pp[i];
+    const double tot = block_sum<NT>(part, red);
+    if (threadIdx.x == 0) {
+      const uint32_t n_s = a.tmpl[b].n_steps;
+      a.delta[b] = n_s ? tot / static_cast<double>(n_s) : 0.0;
+    }
+  }
 }
 
 // ------------------------------------------------------------------ pass 3
@@ -185,19 +196,25 @@ __device__ __forceinline__ float2 padding_spectrum(const TwiddleTable& tw, uint3
 
 // Per-row constants: bin k = c + C k3 factors as W_2N^{x k} = W_2N^{x c} * W_{4 L3}^{x k3}
 struct RowTw {
-  float2 w;   // W_N^c       (untangle)
   float2 t1;  // W_2N^c
   float2 ta;  // W_2N^{n_s c}
-  float2 tc;  // W_2N^{(n_s-1) c}
 };
 
 __device__ __forceinline__ RowTw row_twiddles(const TwiddleTable& tw, uint32_t c, uint32_t n_s) {
   RowTw r;
-  r.w = tw_lookup32(tw, 2u * c);
   r.t1 = tw_lookup32(tw, c);
   r.ta = tw_lookup(tw, static_cast<uint64_t>(n_s) * c);
-  r.tc = tw_lookup(tw, static_cast<uint64_t>(n_s == 0 ? 0 : n_s - 1) * c);
   return r;
+}
+
+// multiply by (-i)^q
+__device__ __forceinline__ float2 rot_mi(float2 a, uint32_t q) {
+  switch (q & 3u) {
+    case 0: return a;
+    case 1: return make_float2(a.y, -a.x);
+    case 2: return make_float2(-a.x, -a.y);
+    default: return make_float2(-a.y, a.x);
+  }
 }
 
 template <int L, int ROWS, int MODE>
@@ -207,12 +224,11 @@ __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Arg
   constexpr int NT = NSLOT * TPC;
   constexpr int L4 = 4 * L;
   using Lay = BlockLayout<L, NSLOT, TPC, true>;
-  // data | stage twiddles W_L | W_{4L} (= W_2N^{C i}) | reduction scratch
-  __shared__ __attribute__((aligned(16))) float2 smem[Lay::kLds + kTwPad<L> + L4 + 16];
+  // data | stage twiddles W_L | W_{4L} (= W_2N^{C i})
+  __shared__ __attribute__((aligned(16))) float2 smem[Lay::kLds + kTwPad<L> + L4];
   float2* data = smem;
   float2* twl = smem + Lay::kLds;
   float2* t4 = twl + kTwPad<L>;
-  double* red = reinterpret_cast<double*>(t4 + L4);
 
   const int b = blockIdx.y;
   const float2* buf = a.buf + static_cast<size_t>(b) * a.M;
@@ -225,21 +241,25 @@ __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Arg
     Lay::coords(threadIdx.x, slot, tj);
     const uint32_t cs = c0 + (slot % ROWS);
     const uint32_t row = (slot < ROWS) ? cs : (a.C - cs) % a.C;
-    const float2* src = buf + row_base(row < a.C ? row : 0, a.L1, a.L2, a.L3);
-    for (int r = tj; r < L; r += TPC) data[Lay::idx(r, slot)] = src[r];
+    const float4* src = reinterpret_cast<const float4*>(buf + row_base(row < a.C ? row : 0, a.L1, a.L2, a.L3));
+    for (int r = tj; r < L / 2; r += TPC) {
+      const float4 v = src[r];
+      data[Lay::idx(2 * r, slot)] = make_float2(v.x, v.y);
+      data[Lay::idx(2 * r + 1, slot)] = make_float2(v.z, v.w);
+    }
   }
   copy_stage_twiddles<L>(twl, a.tb.st3);
-  for (int i = threadIdx.x; i < L4; i += NT) t4[i] = a.tb.p3[i];
-  // mean-padding correction delta = (sum of (sample - mu0)) / n_steps
+  {
+    const float4* t4s = reinterpret_cast<const float4*>(a.tb.p3);
+    float4* t4d = reinterpret_cast<float4*>(t4);
+    for (int i = threadIdx.x; i < L4 / 2; i += NT) t4d[i] = t4s[i];
+  }
+  // mean-padding correction delta = (sum of (sample - mu0)) / n_steps (pass 2)
   double delta = 0.0;
   uint32_t n_s = 0;
   if (MODE == P3_POWER) {
-    double part = 0.0;
-    const double* pp = a.partials + static_cast<size_t>(b) * a.n_partials;
-    for (uint32_t i = threadIdx.x; i < a.n_partials; i += NT) part += pp[i];
-    const double tot = block_sum<NT>(part, red);
     n_s = a.tmpl[b].n_steps;
-    delta = tot / static_cast<double>(n_s);
+    delta = a.delta[b];
   }
   // per-row twiddle constants of the untangle phase, fetched before the FFT so
   // their latency hides under it
@@ -248,48 +268,59 @@ __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Arg
   constexpr int kStreams = NT / ROWS;
   const uint32_t c = c0 + s;
   const uint32_t half = a.C / 2;
-  const uint32_t cm = (a.C - c) % a.C;
   const RowTw rt = row_twiddles(a.tw, c, n_s);
-  const RowTw rm = row_twiddles(a.tw, cm, n_s);
   __syncthreads();
-  BlockFFT<L, NSLOT, TPC, true>::run(data, twl);
+  if (!(a.exp & 4)) BlockFFT<L, NSLOT, TPC, true>::run(data, twl);
+  if (a.exp & 8) {
+    if (data[Lay::idx(t, s)].x == 12345.0f) a.ps[threadIdx.x] = 1.0f;
+    return;
+  }
 
   const float dS = static_cast<float>(delta);
-  const bool correct = (MODE == P3_POWER) && n_s > 0;
-  auto emit = [&](uint32_t k, float2 x, const RowTw& rt, uint32_t k3) {
+  const bool correct = (MODE == P3_POWER) && n_s > 0 && !(a.exp & 2);
+  float sink = 0.0f;
+  float* ps = a.ps + static_cast<size_t>(b) * a.ps_stride;
+  // X_k (+ delta * S_k) -> |X_k|^2 / N, or the complex bin
+  // S_k = -(sin(pi n_s k/N) / sin(pi k/N)) e^{-i pi (n_s-1) k/N} from ta = W_2N^{n_s k}, tk = W_2N^k
+  auto emit = [&](uint32_t k, float2 x, float2 tk, float2 ta) {
     if (k >= a.limit) return;
     if (MODE == P3_POWER) {
       float p = 0.0f;
       if (k != 0) {
         if (correct) {
-          const float2 ta = cmul(rt.ta, t4[(n_s * k3) % L4]);
-          const float2 tk = cmul(rt.t1, t4[k3]);
-          const float2 tc = cmul(rt.tc, t4[((n_s - 1) * k3) % L4]);
-          const float2 s = padding_spectrum_t(ta, tk, tc);
-          x = make_float2(x.x + dS * s.x, x.y + dS * s.y);
+          const float ratio = __fdividef(ta.y, tk.y);
+          const float2 tc = cmul(ta, conjf2(tk));  // W_2N^{(n_s-1) k}
+          x = make_float2(x.x - dS * ratio * tc.x, x.y - dS * ratio * tc.y);
         }
-        const double re = x.x, im = x.y;
-        p = static_cast<float>(static_cast<double>(a.norm) * (re * re + im * im));
+        p = (x.x * x.x + x.y * x.y) * a.norm;
       }
-      a.ps[static_cast<size_t>(b) * a.ps_stride + k] = p;
+      if (a.exp & 1) sink += p;
+      else ps[k] = p;
     } else {
       a.spec[k] = x;
     }
   };
 
-  // untangle: thread -> (slot s, k3 stream), rows c <= C/2 own their bins
+  // untangle: thread -> (slot s, k3 stream), rows c <= C/2 own their bins;
+  // bin M-k of the mirror row reuses the twiddles of bin k:
+  //   W_2N^{M-k} = -i conj(W_2N^k),  W_2N^{n_s (M-k)} = (-i)^{n_s} conj(W_2N^{n_s k})
   if (c <= half) {
     for (int k3 = t; k3 < L; k3 += kStreams) {
       const float2 zk = data[Lay::idx(k3, s)];
       const int k3m = (c == 0) ? (L - k3) % L : L - 1 - k3;
       const float2 zm = data[Lay::idx(k3m, c == 0 ? s : ROWS + s)];
       const uint32_t k = c + a.C * static_cast<uint32_t>(k3);
-      const float2 w = cmul(rt.w, t4[(2 * k3) % L4]);  // W_N^k
-      emit(k, untangle_w(zk, zm, w), rt, static_cast<uint32_t>(k3));
+      const float2 tk = cmul(rt.t1, t4[k3]);  // W_2N^k
+      const float2 w = cmul(tk, tk);          // W_N^k
+      float2 ta = make_float2(0.f, 0.f);
+      if (correct) ta = cmul(rt.ta, t4[(n_s * static_cast<uint32_t>(k3)) % L4]);
+      emit(k, untangle_w(zk, zm, w), tk, ta);
       if (c != 0 && c != half) {
-        const uint32_t kk = a.M - k;  // = cm + C*(L-1-k3)
+        const uint32_t kk = a.M - k;                 // = cm + C*(L-1-k3)
         const float2 wm = make_float2(-w.x, w.y);  // W_N^{M-k} = -conj(W_N^k)
-        emit(kk, untangle_w(zm, zk, wm), rm, static_cast<uint32_t>(L - 1 - k3));
+        const float2 tkm = make_float2(-tk.y, -tk.x);
+        const float2 tam = rot_mi(conjf2(ta), n_s);
+        emit(kk, untangle_w(zm, zk, wm), tkm, tam);
       }
       if (c == 0 && k3 == 0 && a.M < a.limit) {
         // Nyquist bin M: X_M = Re Z_0 - Im Z_0
@@ -299,15 +330,14 @@ __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Arg
             const float2 sp = padding_spectrum(a.tw, n_s, a.M);
             x = make_float2(x.x + dS * sp.x, x.y + dS * sp.y);
           }
-          const double re = x.x, im = x.y;
-          a.ps[static_cast<size_t>(b) * a.ps_stride + a.M] =
-              static_cast<float>(static_cast<double>(a.norm) * (re * re + im * im));
+          ps[a.M] = (x.x * x.x + x.y * x.y) * a.norm;
         } else {
           a.spec[a.M] = x;
         }
       }
     }
   }
+  if ((a.exp & 1) && sink == 12345.0f) a.ps[threadIdx.x] = sink;
 }
 
 template <int L, int ROWS>
