@@ -32,7 +32,7 @@ DATA = ROOT / "data" / "testwu"
 WU = DATA / "p2030.20151015.G187.41-00.88.N.b2s0g0.00000_1099.bin4"
 BANK = DATA / "stochastic_full.bank"
 ZAP = DATA / "p2030.20151015.G187.41-00.88.N.b2s0g0.00000.zap"
-GOLDEN = ROOT / "data" / "golden" / "bench_wu_gpu_results.txt"
+GOLDEN = ROOT / "data" / "golden" / "bench_wu_cpu_results.txt"  # tools/make_golden.py (CPU golden model)
 
 
 def parse():
@@ -40,7 +40,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=int(os.environ.get("BRP_BATCH", "4")))
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("BRP_BATCH", "8")))
+    ap.add_argument("--streams", type=int, default=int(os.environ.get("BRP_STREAMS", "2")),
+                    help="independent pipelines (stream + buffers) per GPU; >1 overlaps host sync with compute")
     ap.add_argument("--templates", type=int, default=0, help="limit the bank (0 = all 6662)")
     ap.add_argument("--synthetic", action="store_true", help="synthetic WU/bank of the benchmark shape")
     ap.add_argument("--write-output", default="", help="rank 0 writes the result file of the last step here")
@@ -92,7 +94,7 @@ def main() -> int:
         data_desc = "synthetic: 2^22-sample 4-bit WU with an injected binary pulsar + random 6662-template bank"
     opts = dict(inputfile=str(wu), templatebank=str(bank), zaplistfile=str(zap), f0=400.0, padding=3.0, fA=0.08,
                 window=1000, white=True, batch=args.batch, outputfile=args.write_output)
-    search = ShardedSearch(opts, ctx)
+    search = ShardedSearch(opts, ctx, streams=args.streams)
     limit = args.templates if args.templates > 0 else search.total
     if torch.cuda.is_available():
         torch.cuda.synchronize()

@@ -122,15 +122,19 @@ def max_over_ranks(value: float, ctx: DistContext) -> float:
 class ShardedSearch:
     """One work unit searched by all ranks: rank r takes templates shard_range(r)."""
 
-    def __init__(self, options: dict, ctx: DistContext, device: int | None = None, use_cpu: bool = False):
+    def __init__(self, options: dict, ctx: DistContext, device: int | None = None, use_cpu: bool = False,
+                 streams: int = 1):
+        """`streams` independent pipelines (HIP stream + buffers) share this rank's
+        GPU: while the host applies one batch's candidates the GPU runs the next."""
         self.brp = native()
         self.ctx = ctx
         self.options = dict(options)
         if use_cpu:
             self.options["use_cpu"] = True
         dev = ctx.local_rank if device is None else device
+        streams = max(1, streams)
         self.session = self.brp.SearchSession()
-        self.session.open(self.options, 1, [] if use_cpu else [dev])
+        self.session.open(self.options, streams, [] if use_cpu else [dev] * streams)
         self.total = self.session.total()
         self.begin, self.end = shard_range(self.total, ctx.rank, ctx.world)
 

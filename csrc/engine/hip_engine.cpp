@@ -281,6 +281,7 @@ struct HipEngine::Impl {
         a2.n_partials = plan.wg1();
         a2.tmpl = tmpl.p;
         a2.delta = delta.p;
+        a2.exp = p3_exp;
         return hipk::launch_pass2(plan, a2, nb, stream);
       }
       case kPass3: {

@@ -70,6 +70,7 @@ struct Pass2Args {
   uint32_t n_partials;
   const TemplateDev* tmpl;
   double* delta;               // [batch]
+  uint32_t exp;                // profiling experiments (BRP_P3_EXP), 0 in production
 };
 
 enum Pass3Mode : int {

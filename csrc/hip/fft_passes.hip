@@ -140,17 +140,23 @@ __global__ void __launch_bounds__(kNcol * tpc_for<L>()) pass2_kernel(Pass2Args a
   Lay::coords(threadIdx.x, c, tj);
   for (int r = tj; r < L; r += TPC) data[Lay::idx(r, c)] = buf[base + static_cast<size_t>(r) * a.L3 + c];
   // W_M^{n3 (k1 + L1 k2)} = W_M^{n3 k1} * W_{L2 L3}^{n3 k2}
-  copy_stage_twiddles<L>(twl, a.tb.st2);
-  const uint32_t nhi = (a.L2L3 + kLo - 1) / kLo;
-  for (int i = threadIdx.x; i < kNcol; i += NT) colw[i] = a.tb.p2col[k1 * a.L3 + n3_0 + i];
-  for (int i = threadIdx.x; i < kLo; i += NT) lo[i] = a.tb.p2lo[i];
-  for (uint32_t i = threadIdx.x; i < nhi; i += NT) hi[i] = a.tb.p2hi[i];
+  if (!(a.exp & 64)) {
+    copy_stage_twiddles<L>(twl, a.tb.st2);
+    const uint32_t nhi = (a.L2L3 + kLo - 1) / kLo;
+    for (int i = threadIdx.x; i < kNcol; i += NT) colw[i] = a.tb.p2col[k1 * a.L3 + n3_0 + i];
+    for (int i = threadIdx.x; i < kLo; i += NT) lo[i] = a.tb.p2lo[i];
+    for (uint32_t i = threadIdx.x; i < nhi; i += NT) hi[i] = a.tb.p2hi[i];
+  }
   __syncthreads();
-  BlockFFT<L, kNcol, TPC, false>::run(data, twl);
+  if (!(a.exp & 16)) BlockFFT<L, kNcol, TPC, false>::run(data, twl);
   const uint32_t n3 = n3_0 + c;
   const float2 wc = colw[c];
   for (int k2 = tj; k2 < L; k2 += TPC) {
     const uint32_t e = n3 * static_cast<uint32_t>(k2);  // < L2*L3
+    if (a.exp & 32) {
+      buf[base + static_cast<size_t>(k2) * a.L3 + c] = data[Lay::idx(k2, c)];
+      continue;
+    }
     const float2 w = cmul(wc, cmul(hi[e >> kP2LoBits], lo[e & (kLo - 1)]));
     buf[base + static_cast<size_t>(k2) * a.L3 + c] = cmul(data[Lay::idx(k2, c)], w);
   }
