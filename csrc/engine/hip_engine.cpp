@@ -147,8 +147,8 @@ struct HipEngine::Impl {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   int batch = 4;
-  uint32_t cap = 1u << 16;      // candidate slots per (template, level)
-  uint32_t kcopy = 2048;        // slots copied back eagerly
+  uint32_t cap = 1u << 20;      // candidate slots per batch (all templates and levels)
+  uint32_t kcopy = 1024;        // slots copied back with every batch (more: second copy)
 
   SearchGeometry g;
   FFTPlan3 plan;
@@ -163,17 +163,19 @@ struct HipEngine::Impl {
   DevBuf<float> ps;             // [batch][ps_stride]
   DevBuf<double> partials;      // [batch][wg1]
   DevBuf<double> delta;         // [batch] mean-padding correction
-  DevBuf<TemplateDev> tmpl;     // [batch]
-  DevBuf<float> thr;            // [5]
-  DevBuf<uint32_t> counts;      // [batch][5]
-  DevBuf<uint2> cands;          // [batch][5][cap]
+  // per-batch input, ONE host->device copy: thresholds | templates
+  DevBuf<uint8_t> in;
+  struct { TemplateDev* p = nullptr; } tmpl;  // views into `in`
+  struct { float* p = nullptr; } thr;
+  DevBuf<uint2> cands;          // [1 + cap]: count | (packed key, power) entries
   DevBuf<float2> tw_hi, tw_lo;
   DevBuf<float2> t_st1, t_st2, t_st3, t_p1, t_p2col, t_p2lo, t_p2hi, t_p3;
 
-  PinnedBuf<TemplateDev> h_tmpl;
-  PinnedBuf<float> h_thr;
-  PinnedBuf<uint32_t> h_counts;
-  PinnedBuf<uint2> h_cands;     // [batch][5][kcopy]
+  PinnedBuf<uint8_t> h_in;
+  struct { TemplateDev* p = nullptr; } h_tmpl;
+  struct { float* p = nullptr; } h_thr;
+  PinnedBuf<uint2> h_cands;     // [1 + kcopy]
+  static constexpr size_t kThrBytes = 64;  // thresholds area at the start of `in`
 
   std::map<int, hipGraphExec_t> graphs;
   BackendStats st;
@@ -249,13 +251,9 @@ struct HipEngine::Impl {
     const hipk::TwiddleTable tw = twt();
     switch (st) {
       case kPrologue:
-        e = hipMemcpyAsync(tmpl.p, h_tmpl.p, sizeof(TemplateDev) * nb, hipMemcpyHostToDevice, stream);
+        e = hipMemcpyAsync(in.p, h_in.p, kThrBytes + sizeof(TemplateDev) * nb, hipMemcpyHostToDevice, stream);
         if (e != hipSuccess) return e;
-        e = hipMemcpyAsync(thr.p, h_thr.p, sizeof(float) * kNumHarmonicLevels, hipMemcpyHostToDevice, stream);
-        if (e != hipSuccess) return e;
-        e = hipMemsetAsync(counts.p, 0, sizeof(uint32_t) * kNumHarmonicLevels * nb, stream);
-        if (e != hipSuccess) return e;
-        return hipk::launch_nsteps(tmpl.p, nb, stream);
+        return hipk::launch_nsteps(tmpl.p, nb, stream, &cands.p[0].x);
       case kPass1: {
         hipk::Pass1Args a1{};
         a1.out = buf.p;
@@ -312,18 +310,12 @@ struct HipEngine::Impl {
         ah.hhi = std::min(g.harmonic_idx_hi, g.fft_size);
         ah.i_start = i_start;
         ah.thr = thr.p;
-        ah.counts = counts.p;
-        ah.cands = cands.p;
+        ah.list = cands.p;
         ah.cap = cap;
         return hipk::launch_harmonic_sum(ah, nb, stream);
       }
       case kEpilogue:
-        e = hipMemcpyAsync(h_counts.p, counts.p, sizeof(uint32_t) * kNumHarmonicLevels * nb, hipMemcpyDeviceToHost,
-                           stream);
-        if (e != hipSuccess) return e;
-        return hipMemcpy2DAsync(h_cands.p, sizeof(uint2) * kcopy, cands.p, sizeof(uint2) * cap,
-                                sizeof(uint2) * kcopy, static_cast<size_t>(kNumHarmonicLevels) * nb,
-                                hipMemcpyDeviceToHost, stream);
+        return hipMemcpyAsync(h_cands.p, cands.p, sizeof(uint2) * (1 + kcopy), hipMemcpyDeviceToHost, stream);
       default: return hipErrorInvalidValue;
     }
   }
@@ -397,14 +389,20 @@ int HipEngine::setup(const SearchGeometry& g, const std::vector<float>& series, 
   if ((rc = d.ps.alloc(B * d.ps_stride))) return rc;
   if ((rc = d.partials.alloc(B * d.plan.wg1()))) return rc;
   if ((rc = d.delta.alloc(B))) return rc;
-  if ((rc = d.tmpl.alloc(B))) return rc;
-  if ((rc = d.thr.alloc(kNumHarmonicLevels))) return rc;
-  if ((rc = d.counts.alloc(B * kNumHarmonicLevels))) return rc;
-  if ((rc = d.cands.alloc(B * kNumHarmonicLevels * d.cap))) return rc;
-  if ((rc = d.h_tmpl.alloc(B))) return rc;
-  if ((rc = d.h_thr.alloc(kNumHarmonicLevels))) return rc;
-  if ((rc = d.h_counts.alloc(B * kNumHarmonicLevels))) return rc;
-  if ((rc = d.h_cands.alloc(B * kNumHarmonicLevels * d.kcopy))) return rc;
+  if (B > hipk::kHsMaxBatch || g.fundamental_idx_hi >= (1u << hipk::kHsBinBits)) {
+    log_message(LOG_ERROR, true, "Batch %zu / fundamental_idx_hi %u beyond the candidate key packing.\n", B,
+                g.fundamental_idx_hi);
+    return RADPUL_EVAL;
+  }
+  const size_t in_bytes = Impl::kThrBytes + sizeof(TemplateDev) * B;
+  if ((rc = d.in.alloc(in_bytes))) return rc;
+  d.thr.p = reinterpret_cast<float*>(d.in.p);
+  d.tmpl.p = reinterpret_cast<TemplateDev*>(d.in.p + Impl::kThrBytes);
+  if ((rc = d.cands.alloc(1 + d.cap))) return rc;
+  if ((rc = d.h_in.alloc(in_bytes))) return rc;
+  d.h_thr.p = reinterpret_cast<float*>(d.h_in.p);
+  d.h_tmpl.p = reinterpret_cast<TemplateDev*>(d.h_in.p + Impl::kThrBytes);
+  if ((rc = d.h_cands.alloc(1 + d.kcopy))) return rc;
   std::vector<float2> hi, lo;
   build_twiddles(4ull * d.plan.M, hi, lo);
   if ((rc = d.tw_hi.alloc(hi.size()))) return rc;
@@ -593,35 +591,35 @@ int HipEngine::process(const TemplateInput* t, int n, const float thr[kNumHarmon
     d.st.gpu_ms += ms;
     d.st.batches += 1;
     d.st.templates += nb;
-    for (int k = 0; k < nb; ++k) {
-      TemplateCands& tc = out[off + k];
+    const uint32_t cnt = d.h_cands.p[0].x;
+    if (cnt > d.cap) {
+      log_message(LOG_ERROR, true, "Candidate overflow (%u > %u slots) in a batch of %d templates.\n", cnt, d.cap, nb);
+      return RADPUL_HIP_CAND_OVERFLOW;
+    }
+    const uint2* src = d.h_cands.p + 1;
+    std::vector<uint2> extra;
+    if (cnt > d.kcopy) {
+      extra.resize(cnt);
+      BRP_HIP_CHECK(hipMemcpy(extra.data(), d.cands.p + 1, cnt * sizeof(uint2), hipMemcpyDeviceToHost),
+                    RADPUL_HIP_MEM_COPY_DEVICE_HOST);
+      src = extra.data();
+      d.st.overflow_reruns += 1;
+    }
+    for (int k = 0; k < nb; ++k)
+      for (int h = 0; h < kNumHarmonicLevels; ++h) out[off + k].level[h].clear();
+    constexpr uint32_t kBinMask = (1u << hipk::kHsBinBits) - 1u;
+    for (uint32_t q = 0; q < cnt; ++q) {
+      const uint32_t key = src[q].x;
+      const uint32_t k = key >> 26, h = (key >> hipk::kHsBinBits) & 7u;
+      float p;
+      std::memcpy(&p, &src[q].y, sizeof(float));
+      out[off + k].level[h].push_back(BinPower{key & kBinMask, p});
+    }
+    for (int k = 0; k < nb; ++k)
       for (int h = 0; h < kNumHarmonicLevels; ++h) {
-        const uint32_t cnt = d.h_counts.p[k * kNumHarmonicLevels + h];
-        std::vector<BinPower>& lv = tc.level[h];
-        lv.clear();
-        if (cnt > d.cap) {
-          log_message(LOG_ERROR, true, "Candidate overflow (%u > %u) on level %d.\n", cnt, d.cap, h);
-          return RADPUL_HIP_CAND_OVERFLOW;
-        }
-        const uint2* src = d.h_cands.p + (static_cast<size_t>(k) * kNumHarmonicLevels + h) * d.kcopy;
-        std::vector<uint2> extra;
-        if (cnt > d.kcopy) {
-          extra.resize(cnt);
-          const uint2* dsrc = d.cands.p + (static_cast<size_t>(k) * kNumHarmonicLevels + h) * d.cap;
-          BRP_HIP_CHECK(hipMemcpy(extra.data(), dsrc, cnt * sizeof(uint2), hipMemcpyDeviceToHost),
-                        RADPUL_HIP_MEM_COPY_DEVICE_HOST);
-          src = extra.data();
-          d.st.overflow_reruns += 1;
-        }
-        lv.resize(cnt);
-        for (uint32_t q = 0; q < cnt; ++q) {
-          float p;
-          std::memcpy(&p, &src[q].y, sizeof(float));
-          lv[q] = BinPower{src[q].x, p};
-        }
+        std::vector<BinPower>& lv = out[off + k].level[h];
         std::sort(lv.begin(), lv.end(), [](const BinPower& a, const BinPower& b) { return a.bin < b.bin; });
       }
-    }
   }
   return 0;
 }
@@ -717,8 +715,7 @@ int HipEngine::benchmark_stages(const TemplateInput* t, int n, int reps, std::ve
         // the harmonic stage appends to the candidate lists: reset their
         // counters (a 100-byte memset) so every repetition sees the same load
         if (st == Impl::kHarmonic)
-          BRP_HIP_CHECK(hipMemsetAsync(d.counts.p, 0, sizeof(uint32_t) * kNumHarmonicLevels * nb, d.stream),
-                        RADPUL_HIP_KERNEL_INVOKE);
+          BRP_HIP_CHECK(hipMemsetAsync(d.cands.p, 0, sizeof(uint2), d.stream), RADPUL_HIP_KERNEL_INVOKE);
         BRP_HIP_CHECK(d.enqueue_stage(st, nb), RADPUL_HIP_KERNEL_INVOKE);
       }
     }

@@ -28,7 +28,7 @@ constexpr int kSpan = kHsTile + kHalo;
 constexpr int kSpanPad = kSpan + kSpan / 16 + 1;
 __device__ __forceinline__ int sidx(int t) { return t + (t >> 4); }
 
-__device__ __forceinline__ void emit(uint32_t* counter, uint2* list, uint32_t cap, bool pred, uint32_t bin,
+__device__ __forceinline__ void emit(uint32_t* counter, uint2* list, uint32_t cap, bool pred, uint32_t key,
                                      float power) {
   const unsigned long long mask = __ballot(pred);
   if (mask == 0) return;
@@ -40,7 +40,7 @@ __device__ __forceinline__ void emit(uint32_t* counter, uint2* list, uint32_t ca
   if (pred) {
     const uint32_t rank = __popcll(mask & ((1ull << lane) - 1ull));
     const uint32_t slot = base + rank;
-    if (slot < cap) list[slot] = make_uint2(bin, __float_as_uint(power));
+    if (slot < cap) list[slot] = make_uint2(key, __float_as_uint(power));
   }
 }
 
@@ -74,15 +74,15 @@ __global__ void __launch_bounds__(kThreads) harmonic_sum_kernel(HSArgs a) {
   }
   __syncthreads();
 
-  uint32_t* counts = a.counts + static_cast<size_t>(b) * 5;
-  uint2* cands = a.cands + static_cast<size_t>(b) * 5 * a.cap;
+  uint32_t* count = &a.list[0].x;
+  uint2* list = a.list + 1;
   const float thr0 = a.thr[0];
   // level 0: the power spectrum itself
   for (int t = threadIdx.x; t < kHsTile; t += kThreads) {
     const uint32_t i = i0 + t;
     const bool in = (i >= a.w2 && i < a.fhi);
     const float p = in ? P[i] : 0.0f;
-    emit(&counts[0], cands, a.cap, in && p > thr0, i, p);
+    emit(count, list, a.cap, in && p > thr0, hs_pack(b, 0, i), p);
   }
   // levels 1..4: group of 2^h consecutive i starting at s == 2^(h-1) mod 2^h;
   // one thread per group, stride-2^h reads made (nearly) conflict free by the
@@ -108,7 +108,7 @@ __global__ void __launch_bounds__(kThreads) harmonic_sum_kernel(HSArgs a) {
           pred = m > thr;
         }
       }
-      emit(&counts[h], cands + static_cast<size_t>(h) * a.cap, a.cap, pred, j, m);
+      emit(count, list, a.cap, pred, hs_pack(b, h, j), m);
     }
   }
 }

@@ -16,10 +16,17 @@ struct HSArgs {
   uint32_t w2, fhi, hhi;  // window_2, fundamental_idx_hi, harmonic_idx_hi
   uint32_t i_start;       // first i of tile 0 (== 8 mod 16, <= w2)
   const float* thr;       // [5] device thresholds for the whole batch
-  uint32_t* counts;       // [batch][5] (atomic; may exceed cap)
-  uint2* cands;           // [batch][5][cap]: (bin, power bits)
+  // one compact list per batch: list[0].x = number of entries (atomic; may
+  // exceed cap), list[1 + q] = (hs_pack(template, level, bin), power bits)
+  uint2* list;
   uint32_t cap;
 };
+
+constexpr uint32_t kHsBinBits = 23;  // bins < 2^23, levels < 8, templates per batch < 64
+constexpr uint32_t kHsMaxBatch = 64;
+__host__ __device__ constexpr uint32_t hs_pack(uint32_t k, uint32_t h, uint32_t bin) {
+  return (k << 26) | (h << kHsBinBits) | bin;
+}
 
 uint32_t hs_num_tiles(uint32_t i_start, uint32_t hhi);
 hipError_t launch_harmonic_sum(const HSArgs& a, int batch, hipStream_t s);

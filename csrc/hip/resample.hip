@@ -16,8 +16,9 @@ namespace {
 
 constexpr int kThreads = 256;
 
-__global__ void __launch_bounds__(kThreads) nsteps_kernel(TemplateDev* tmpl) {
+__global__ void __launch_bounds__(kThreads) nsteps_kernel(TemplateDev* tmpl, uint32_t* reset) {
   __shared__ uint32_t best;
+  if (reset != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *reset = 0;
   TemplateDev& td = tmpl[blockIdx.x];
   const ResampParams p = td.p;
   const uint32_t nu = p.nsamples_unpadded;
@@ -59,8 +60,8 @@ __global__ void resample_kernel(const float* series, uint32_t n_unpadded, const 
 
 }  // namespace
 
-hipError_t launch_nsteps(TemplateDev* tmpl, int batch, hipStream_t s) {
-  hipLaunchKernelGGL(nsteps_kernel, dim3(batch), dim3(kThreads), 0, s, tmpl);
+hipError_t launch_nsteps(TemplateDev* tmpl, int batch, hipStream_t s, uint32_t* reset) {
+  hipLaunchKernelGGL(nsteps_kernel, dim3(batch), dim3(kThreads), 0, s, tmpl, reset);
   return hipGetLastError();
 }
 

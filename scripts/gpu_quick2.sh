@@ -1,0 +1,11 @@
+# GPU tests + stage timings + a short bench
+set -o pipefail
+export TMPDIR=/tmp
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+timeout -k 10 600 python -m pytest tests -q -m gpu -x > gpurun_out/tests_all.log 2>&1 || { echo TEST_FAIL; tail -60 gpurun_out/tests_all.log; exit 1; }
+tail -1 gpurun_out/tests_all.log
+timeout -k 10 120 python tools/stagebench.py 4 > gpurun_out/stage.log 2>&1 || { echo STAGE_FAIL; tail -20 gpurun_out/stage.log; exit 1; }
+tail -1 gpurun_out/stage.log
+timeout -k 10 300 python bench.py --steps 3 --warmup 1 > gpurun_out/bench.log 2>&1 || { echo BENCH_FAIL; tail -20 gpurun_out/bench.log; exit 1; }
+tail -1 gpurun_out/bench.log
