@@ -66,6 +66,15 @@ BRP_HD inline int resamp_nearest(uint32_t i, float del_t) {
   return static_cast<int>(static_cast<double>(x) + 0.5);
 }
 
+// Same result as resamp_nearest without double arithmetic, valid for
+// |x| < 2^23: there float(x) + 0.5f is exact (ulp(x) <= 0.5), so both round
+// trips truncate the same value. Callers guarantee i < n_unpadded <= 2^23.
+BRP_HD inline int resamp_nearest_f(uint32_t i, float del_t) {
+#pragma clang fp contract(off)
+  const float x = static_cast<float>(i) - del_t;
+  return static_cast<int>(x + 0.5f);
+}
+
 // True if sample m must be dropped at the end of the series
 // (reference loop `while(n_steps - del_t[n_steps] >= N_u - 1) n_steps--`).
 BRP_HD inline bool resamp_beyond_end(uint32_t m, float del_t, uint32_t n_unpadded) {

@@ -155,6 +155,8 @@ struct HipEngine::Impl {
   bool ready = false;
   float mu0 = 0.0f;
   uint32_t p3_exp = 0;          // BRP_P3_EXP profiling switches (pass3_kernel)
+  uint32_t num_cus = 256;
+  uint32_t persist_per_cu = 4;  // persistent FFT passes: workgroups per CU (BRP_PERSIST, 0 = off)
   uint32_t ps_stride = 0;
   uint32_t i_start = 0;
 
@@ -265,6 +267,7 @@ struct HipEngine::Impl {
         a1.n_unpadded = g.n_unpadded;
         a1.tmpl = tmpl.p;
         a1.partials = partials.p;
+        a1.exp = p3_exp;
         return hipk::launch_pass1(plan, hipk::P1_RESAMPLE, a1, nb, stream);
       }
       case kPass2: {
@@ -361,6 +364,7 @@ int HipEngine::init(int device, int batch) {
   BRP_HIP_CHECK(hipGetDeviceProperties(&prop, device), RADPUL_HIP_DEVICE_PROP);
   log_message(LOG_INFO, true, "Using HIP device #%d: %s (%s, %d CUs, %.1f GB)\n", device, prop.name,
               prop.gcnArchName, prop.multiProcessorCount, prop.totalGlobalMem / 1e9);
+  impl_->num_cus = static_cast<uint32_t>(prop.multiProcessorCount);
   return 0;
 }
 
@@ -376,6 +380,8 @@ int HipEngine::setup(const SearchGeometry& g, const std::vector<float>& series, 
                 g.nsamples);
     return RADPUL_HIP_FFT_PLAN;
   }
+  if (const char* e = std::getenv("BRP_PERSIST")) d.persist_per_cu = static_cast<uint32_t>(std::atoi(e));
+  d.plan.persist_wgs = d.persist_per_cu * d.num_cus;
   log_message(LOG_DEBUG, true, "FFT plan: N=%u M=%u = %u x %u x %u\n", g.nsamples, d.plan.M, d.plan.L1, d.plan.L2,
               d.plan.L3);
   const uint32_t limit = std::min(g.harmonic_idx_hi, g.fft_size);
@@ -600,8 +606,11 @@ int HipEngine::process(const TemplateInput* t, int n, const float thr[kNumHarmon
     std::vector<uint2> extra;
     if (cnt > d.kcopy) {
       extra.resize(cnt);
-      BRP_HIP_CHECK(hipMemcpy(extra.data(), d.cands.p + 1, cnt * sizeof(uint2), hipMemcpyDeviceToHost),
+      // stream-ordered (a null-stream copy would invalidate another engine's
+      // graph capture running in a sibling thread)
+      BRP_HIP_CHECK(hipMemcpyAsync(extra.data(), d.cands.p + 1, cnt * sizeof(uint2), hipMemcpyDeviceToHost, d.stream),
                     RADPUL_HIP_MEM_COPY_DEVICE_HOST);
+      BRP_HIP_CHECK(hipStreamSynchronize(d.stream), RADPUL_HIP_MEM_COPY_DEVICE_HOST);
       src = extra.data();
       d.st.overflow_reruns += 1;
     }

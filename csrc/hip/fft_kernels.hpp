@@ -56,6 +56,7 @@ struct Pass1Args {
   uint32_t n_real;
   // P1_COMPLEX_CONJ
   const float2* cplx_in;
+  uint32_t exp;                // profiling experiments (BRP_P3_EXP), 0 in production
 };
 
 struct Pass2Args {

@@ -8,6 +8,8 @@
 // clFFT / FFTW calls (cuda/app/demod_binary_cuda.cu:849-965,
 // opencl/app/demod_binary_ocl.cpp:972-1314, demod_binary_fft_fftw.c:46-113) and
 // its resampling kernels (cuda/app/demod_binary_cuda.cuh:69-184).
+#include <algorithm>
+
 #include "fft_block.hpp"
 #include "fft_kernels.hpp"
 
@@ -39,11 +41,15 @@ __device__ __forceinline__ double block_sum(double v, double* scratch) {
   return t;
 }
 
+
+// One resampled sample (0 beyond n_steps). `lut` = LDS copy of the sine/cosine
+// tables; `fast` selects the float nearest-index path (n_unpadded <= 2^23).
 __device__ __forceinline__ float resample_sample(uint32_t m, const TemplateDev& td, const float* series,
-                                                 uint32_t n_unpadded) {
+                                                 uint32_t n_unpadded, const float* lut_s, const float* lut_c,
+                                                 bool fast) {
   if (m >= td.n_steps) return 0.0f;
-  const float dt = resamp_del_t(m, td.p, kSinLut, kCosLut);
-  int idx = resamp_nearest(m, dt);
+  const float dt = resamp_del_t(m, td.p, lut_s, lut_c);
+  int idx = fast ? resamp_nearest_f(m, dt) : resamp_nearest(m, dt);
   idx = idx < 0 ? 0 : (idx >= static_cast<int>(n_unpadded) ? static_cast<int>(n_unpadded) - 1 : idx);
   return series[idx] - td.mu0;
 }
@@ -72,12 +78,19 @@ __global__ void __launch_bounds__(kNcol * tpc_for<L>()) pass1_kernel(Pass1Args a
 
   double sum = 0.0;
   if (MODE == P1_RESAMPLE) {
+    __shared__ float lut_s[kLutSize], lut_c[kLutSize];
+    for (int i = threadIdx.x; i < kLutSize; i += NT) {
+      lut_s[i] = kSinLut[i];
+      lut_c[i] = kCosLut[i];
+    }
+    __syncthreads();
+    const bool fast = a.n_unpadded <= (1u << 23);
     const TemplateDev td = a.tmpl[b];
 #pragma unroll 4
     for (int r = tj; r < L; r += TPC) {
       const uint32_t n = r * a.L2L3 + col_base + c;
-      const float x0 = resample_sample(2 * n, td, a.series, a.n_unpadded);
-      const float x1 = resample_sample(2 * n + 1, td, a.series, a.n_unpadded);
+      const float x0 = resample_sample(2 * n, td, a.series, a.n_unpadded, lut_s, lut_c, fast);
+      const float x1 = resample_sample(2 * n + 1, td, a.series, a.n_unpadded, lut_s, lut_c, fast);
       sum += static_cast<double>(x0) + static_cast<double>(x1);
       data[Lay::idx(r, c)] = make_float2(x0, x1);
     }
@@ -111,65 +124,93 @@ __global__ void __launch_bounds__(kNcol * tpc_for<L>()) pass1_kernel(Pass1Args a
 }
 
 // ------------------------------------------------------------------ pass 2
+// at least kMinWaves waves per SIMD: keeps the unrolled prefetch + FFT code
+// within 256 VGPRs (no spills) at 2 waves/SIMD
+constexpr int kMinWaves = 2;
+
 constexpr int kP2LoBits = 8;
 
+// Persistent: each workgroup walks tiles (template b, column k1, 16 columns n3)
+// blockIdx.x, +gridDim.x, ...; the next tile's columns are loaded into
+// registers while the current one is transformed and stored, and the fixed
+// twiddle tables are staged in LDS once per workgroup.
 template <int L>
-__global__ void __launch_bounds__(kNcol * tpc_for<L>()) pass2_kernel(Pass2Args a) {
+__global__ void __launch_bounds__(kNcol * tpc_for<L>(), kMinWaves) pass2_kernel(Pass2Args a, uint32_t ntiles) {
   constexpr int TPC = tpc_for<L>();
   constexpr int NT = kNcol * TPC;
+  constexpr int kPer = L / TPC;
   using Lay = BlockLayout<L, kNcol, TPC, false>;
   constexpr int kLo = 1 << kP2LoBits;
   constexpr int kHiMax = 512;  // L2*L3 <= 2^17
-  // data | stage twiddles | column twiddles W_M^{n3 k1} | W_{L2L3} lo | W_{L2L3} hi
-  __shared__ __attribute__((aligned(16))) float2 smem[Lay::kLds + kTwPad<L> + kNcol + kLo + kHiMax];
+  // data | stage twiddles | W_{L2L3} lo | W_{L2L3} hi
+  __shared__ __attribute__((aligned(16))) float2 smem[Lay::kLds + kTwPad<L> + kLo + kHiMax];
+  __shared__ double red[NT / kWave + 1];
   float2* data = smem;
   float2* twl = smem + Lay::kLds;
-  float2* colw = twl + kTwPad<L>;
-  float2* lo = colw + kNcol;
+  float2* lo = twl + kTwPad<L>;
   float2* hi = lo + kLo;
 
-  const int b = blockIdx.y;
   const uint32_t nblk3 = a.L3 / kNcol;
-  const uint32_t k1 = blockIdx.x / nblk3;
-  const uint32_t n3_0 = (blockIdx.x % nblk3) * kNcol;
+  const uint32_t per_b = a.L1 * nblk3;
   const size_t M = static_cast<size_t>(a.L1) * a.L2L3;
-  float2* buf = a.buf + static_cast<size_t>(b) * M;
-  const size_t base = static_cast<size_t>(k1) * a.L2L3 + n3_0;
-
   int c, tj;
   Lay::coords(threadIdx.x, c, tj);
-  for (int r = tj; r < L; r += TPC) data[Lay::idx(r, c)] = buf[base + static_cast<size_t>(r) * a.L3 + c];
-  // W_M^{n3 (k1 + L1 k2)} = W_M^{n3 k1} * W_{L2 L3}^{n3 k2}
+  auto tile_base = [&](uint32_t tl) -> size_t {
+    const uint32_t b = tl / per_b, rem = tl % per_b;
+    return static_cast<size_t>(b) * M + static_cast<size_t>(rem / nblk3) * a.L2L3 + (rem % nblk3) * kNcol;
+  };
+
+  float2 pre[kPer];
+  uint32_t tile = blockIdx.x;
+  if (tile < ntiles) {
+    const float2* src = a.buf + tile_base(tile);
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) pre[u] = src[static_cast<size_t>(tj + u * TPC) * a.L3 + c];
+  }
   if (!(a.exp & 64)) {
     copy_stage_twiddles<L>(twl, a.tb.st2);
     const uint32_t nhi = (a.L2L3 + kLo - 1) / kLo;
-    for (int i = threadIdx.x; i < kNcol; i += NT) colw[i] = a.tb.p2col[k1 * a.L3 + n3_0 + i];
     for (int i = threadIdx.x; i < kLo; i += NT) lo[i] = a.tb.p2lo[i];
     for (uint32_t i = threadIdx.x; i < nhi; i += NT) hi[i] = a.tb.p2hi[i];
   }
-  __syncthreads();
-  if (!(a.exp & 16)) BlockFFT<L, kNcol, TPC, false>::run(data, twl);
-  const uint32_t n3 = n3_0 + c;
-  const float2 wc = colw[c];
-  for (int k2 = tj; k2 < L; k2 += TPC) {
-    const uint32_t e = n3 * static_cast<uint32_t>(k2);  // < L2*L3
-    if (a.exp & 32) {
-      buf[base + static_cast<size_t>(k2) * a.L3 + c] = data[Lay::idx(k2, c)];
-      continue;
+  while (tile < ntiles) {
+    const uint32_t b = tile / per_b, rem = tile % per_b;
+    const uint32_t k1 = rem / nblk3;
+    const uint32_t n3 = (rem % nblk3) * kNcol + c;
+    float2* base = a.buf + tile_base(tile);
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) data[Lay::idx(tj + u * TPC, c)] = pre[u];
+    // W_M^{n3 (k1 + L1 k2)} = W_M^{n3 k1} * W_{L2 L3}^{n3 k2}
+    const float2 wc = a.tb.p2col[k1 * a.L3 + n3];
+    const uint32_t next = tile + gridDim.x;
+    if (next < ntiles) {  // in flight during this tile's FFT and stores
+      const float2* src = a.buf + tile_base(next);
+#pragma unroll
+      for (int u = 0; u < kPer; ++u) pre[u] = src[static_cast<size_t>(tj + u * TPC) * a.L3 + c];
     }
-    const float2 w = cmul(wc, cmul(hi[e >> kP2LoBits], lo[e & (kLo - 1)]));
-    buf[base + static_cast<size_t>(k2) * a.L3 + c] = cmul(data[Lay::idx(k2, c)], w);
-  }
-  if (a.partials != nullptr && blockIdx.x == 0) {
-    __shared__ double red[NT / kWave + 1];
-    const double* pp = a.partials + static_cast<size_t>(b) * a.n_partials;
-    double part = 0.0;
-    for (uint32_t i = threadIdx.x; i < a.n_partials; i += NT) part += pp[i];
-    const double tot = block_sum<NT>(part, red);
-    if (threadIdx.x == 0) {
-      const uint32_t n_s = a.tmpl[b].n_steps;
-      a.delta[b] = n_s ? tot / static_cast<double>(n_s) : 0.0;
+    __syncthreads();
+    if (!(a.exp & 16)) BlockFFT<L, kNcol, TPC, false>::run(data, twl);
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int k2 = tj + u * TPC;
+      const uint32_t e = n3 * static_cast<uint32_t>(k2);  // < L2*L3
+      float2 v = data[Lay::idx(k2, c)];
+      if (!(a.exp & 32)) v = cmul(v, cmul(wc, cmul(hi[e >> kP2LoBits], lo[e & (kLo - 1)])));
+      base[static_cast<size_t>(k2) * a.L3 + c] = v;
     }
+    if (a.partials != nullptr && rem == 0) {
+      // mean-padding correction of template b, reduced once in a fixed order
+      const double* pp = a.partials + static_cast<size_t>(b) * a.n_partials;
+      double part = 0.0;
+      for (uint32_t i = threadIdx.x; i < a.n_partials; i += NT) part += pp[i];
+      const double tot = block_sum<NT>(part, red);
+      if (threadIdx.x == 0) {
+        const uint32_t n_s = a.tmpl[b].n_steps;
+        a.delta[b] = n_s ? tot / static_cast<double>(n_s) : 0.0;
+      }
+    }
+    __syncthreads();  // LDS tile free for the next iteration
+    tile = next;
   }
 }
 
@@ -425,11 +466,12 @@ hipError_t launch_pass1(const FFTPlan3& plan, Pass1Mode mode, const Pass1Args& a
 }
 
 hipError_t launch_pass2(const FFTPlan3& plan, const Pass2Args& a, int batch, hipStream_t s) {
-  const dim3 grid(plan.wg2(), batch);
+  const uint32_t ntiles = plan.wg2() * static_cast<uint32_t>(batch);
+  const dim3 grid(plan.persist_wgs ? std::min(ntiles, plan.persist_wgs) : ntiles);
   switch (plan.L2) {
 #define X(n)                                                                \
   case n:                                                                   \
-    hipLaunchKernelGGL((pass2_kernel<n>), grid, dim3(kNcol * tpc_for<n>()), 0, s, a); \
+    hipLaunchKernelGGL((pass2_kernel<n>), grid, dim3(kNcol * tpc_for<n>()), 0, s, a, ntiles); \
     break;
     BRP_P12_LENGTHS(X)
 #undef X
