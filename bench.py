@@ -105,6 +105,7 @@ def main() -> int:
     barrier(ctx)
     if torch.cuda.is_available():
         torch.cuda.synchronize()
+    search.timings.clear()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         table = search.step(limit)
@@ -141,6 +142,7 @@ def main() -> int:
             "candidates_in_table": n_cands,
             "gpu_ms_rank0": round(stats["gpu_ms"], 3),
             "whiten_ms_rank0": round(stats["whiten_ms"], 3),
+            "phase_ms_per_step_rank0": {k: round(1e3 * v / args.steps, 2) for k, v in search.timings.items()},
             "config": {
                 "model": "Einstein@Home BRP4 search (-P 3.0 -f 400 -A 0.08 -W): resample + 3*2^22-pt real FFT "
                          "+ 16-harmonic sum + top-100 per level",

@@ -137,15 +137,25 @@ class ShardedSearch:
         self.session.open(self.options, streams, [] if use_cpu else [dev] * streams)
         self.total = self.session.total()
         self.begin, self.end = shard_range(self.total, ctx.rank, ctx.world)
+        self.timings: dict = {}  # accumulated seconds per phase of step()
 
     def step(self, limit: int | None = None):
         """Whiten + search this rank's shard + all-gather + merge. Returns the merged table."""
+        import time
+
         total = self.total if limit is None else min(limit, self.total)
         begin, end = shard_range(total, self.ctx.rank, self.ctx.world)
+        t0 = time.perf_counter()
         self.session.prepare()
+        t1 = time.perf_counter()
         table, _ = self.session.run(begin, end, self.brp.CandidateTable())
+        t2 = time.perf_counter()
         tables = allgather_tables(table, self.ctx)
-        return merge_tables(tables)
+        merged = merge_tables(tables)
+        t3 = time.perf_counter()
+        for k, v in (("prepare", t1 - t0), ("templates", t2 - t1), ("merge", t3 - t2)):
+            self.timings[k] = self.timings.get(k, 0.0) + v
+        return merged
 
     def write_output(self, table, n_done: int | None = None):
         """Rank 0 writes the checkpoint/result files of the merged table."""

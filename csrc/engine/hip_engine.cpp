@@ -171,6 +171,8 @@ struct HipEngine::Impl {
   struct { float* p = nullptr; } thr;
   DevBuf<uint2> cands;          // [1 + cap]: count | (packed key, power) entries
   DevBuf<float2> tw_hi, tw_lo;
+  DevBuf<float2> w_spec, w_z;   // whitening scratch: half spectrum, packed inverse input
+  DevBuf<float> w_psw, w_med;   // whitening scratch: power spectrum, running median
   DevBuf<float2> t_st1, t_st2, t_st3, t_p1, t_p2col, t_p2lo, t_p2hi, t_p3;
 
   PinnedBuf<uint8_t> h_in;
@@ -368,9 +370,27 @@ int HipEngine::init(int device, int batch) {
   return 0;
 }
 
+namespace {
+bool same_geometry(const SearchGeometry& a, const SearchGeometry& b) {
+  return a.nsamples == b.nsamples && a.n_unpadded == b.n_unpadded && a.fft_size == b.fft_size &&
+         a.window_2 == b.window_2 && a.fundamental_idx_hi == b.fundamental_idx_hi &&
+         a.harmonic_idx_hi == b.harmonic_idx_hi && a.dt == b.dt && a.step_inv == b.step_inv;
+}
+}  // namespace
+
 int HipEngine::setup(const SearchGeometry& g, const std::vector<float>& series, float mu0) {
   Impl& d = *impl_;
   BRP_HIP_CHECK(hipSetDevice(d.device), RADPUL_HIP_DEVICE_SET);
+  if (d.ready && same_geometry(d.g, g)) {
+    // next work unit of the same shape (or the same WU again): buffers, tables
+    // and captured graphs stay valid; only the series and its mean change
+    d.g = g;
+    d.mu0 = mu0;
+    BRP_HIP_CHECK(hipMemcpy(d.series.p, series.data(), g.n_unpadded * sizeof(float), hipMemcpyHostToDevice),
+                  RADPUL_HIP_MEM_COPY_HOST_DEVICE);
+    return 0;
+  }
+  d.ready = false;
   for (auto& kv : d.graphs) (void)hipGraphExecDestroy(kv.second);
   d.graphs.clear();
   d.g = g;
@@ -441,13 +461,15 @@ int HipEngine::whiten(const SearchOptions& opt, const std::vector<ZapRange>& zap
   log_message(LOG_INFO, true, "Seed for random number generator is %d.\n", seed);
   const uint32_t fft_size = g.fft_size, M = d.plan.M;
   if (fft_size < opt.window) return RADPUL_EVAL;
-  DevBuf<float2> spec, z;
-  DevBuf<float> psw, med;
+  DevBuf<float2>& spec = d.w_spec;
+  DevBuf<float>& psw = d.w_psw;
+  DevBuf<float>& med = d.w_med;
   int rc;
-  if ((rc = spec.alloc(fft_size))) return rc;
-  if ((rc = psw.alloc(fft_size))) return rc;
   const uint32_t white_size = fft_size - opt.window + 1;
-  if ((rc = med.alloc(white_size))) return rc;
+  // scratch kept across work units of the same shape
+  if (spec.n < fft_size && (rc = spec.alloc(fft_size))) return rc;
+  if (psw.n < fft_size && (rc = psw.alloc(fft_size))) return rc;
+  if (med.n < white_size && (rc = med.alloc(white_size))) return rc;
   float2* work = d.buf.p;  // M complex scratch (batch slot 0)
   const hipk::TwiddleTable tw = d.twt();
   hipStream_t s = d.stream;
@@ -514,7 +536,8 @@ int HipEngine::whiten(const SearchOptions& opt, const std::vector<ZapRange>& zap
     BRP_HIP_CHECK(hipk::launch_zap(spec.p, fft_size, zbins.p, znoise.p, nz, s), RADPUL_HIP_KERNEL_INVOKE);
   }
   // inverse c2r: tangle, conj-FFT, natural order, scale by 1/sqrt(N), keep n_unpadded
-  if ((rc = z.alloc(M))) return rc;
+  DevBuf<float2>& z = d.w_z;
+  if (z.n < M && (rc = z.alloc(M))) return rc;
   BRP_HIP_CHECK(hipk::launch_tangle(spec.p, M, fft_size, g.window_2, tw, z.p, s), RADPUL_HIP_KERNEL_INVOKE);
   a1 = hipk::Pass1Args{};
   a1.out = work;
