@@ -20,30 +20,35 @@ __global__ void whiten_power_kernel(const float2* spec, uint32_t n, float* ps) {
   ps[k] = p;
 }
 
-// Exact running median: each workgroup sorts (value, position) of its span in
-// LDS (bitonic) and every thread walks the sorted span counting the entries of
-// its own window up to the middle order statistics.
-template <int SPAN>
-__global__ void __launch_bounds__(1024) running_median_kernel(const float* in, uint32_t n_in, uint32_t W,
-                                                              float* med, uint32_t n_out, uint32_t per_block) {
+// Exact running median. Each workgroup sorts (value, position) of its span of
+// SPAN inputs in LDS (bitonic; ties by position, a total order, so the order
+// statistics are exactly those of the reference's sorted window) and keeps the
+// inverse permutation rank[position]. Each thread owns a run of consecutive
+// outputs: it finds the middle member of its first window by one scan of the
+// sorted span, then slides the window one sample at a time, moving the median
+// pointer past the removed / inserted ranks (O(1) members per step).
+template <int SPAN, int NT>
+__global__ void __launch_bounds__(NT) running_median_kernel(const float* in, uint32_t n_in, uint32_t W, float* med,
+                                                            uint32_t n_out, uint32_t per_block) {
   __shared__ float key[SPAN];
-  __shared__ uint32_t pos[SPAN];
+  __shared__ uint16_t pos[SPAN];
+  __shared__ uint16_t rank[SPAN];
+  static_assert(SPAN <= 65536, "16-bit positions");
   const uint32_t o0 = blockIdx.x * per_block;
-  for (int t = threadIdx.x; t < SPAN; t += blockDim.x) {
+  for (int t = threadIdx.x; t < SPAN; t += NT) {
     const uint32_t g = o0 + t;
     key[t] = (t < static_cast<int>(per_block + W - 1) && g < n_in) ? in[g] : __builtin_inff();
-    pos[t] = t;
+    pos[t] = static_cast<uint16_t>(t);
   }
   __syncthreads();
-  // bitonic sort ascending by (key, pos)
   for (int size = 2; size <= SPAN; size <<= 1) {
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int t = threadIdx.x; t < SPAN / 2; t += blockDim.x) {
+      for (int t = threadIdx.x; t < SPAN / 2; t += NT) {
         const int lo = 2 * t - (t & (stride - 1));
         const int hi = lo + stride;
         const bool asc = ((lo & size) == 0);
         const float ka = key[lo], kb = key[hi];
-        const uint32_t pa = pos[lo], pb = pos[hi];
+        const uint16_t pa = pos[lo], pb = pos[hi];
         const bool gt = (ka > kb) || (ka == kb && pa > pb);
         if (gt == asc) {
           key[lo] = kb;
@@ -55,30 +60,55 @@ __global__ void __launch_bounds__(1024) running_median_kernel(const float* in, u
       __syncthreads();
     }
   }
-  const uint32_t mid = (W + (W & 1)) / 2 - 1;
+  for (int e = threadIdx.x; e < SPAN; e += NT) rank[pos[e]] = static_cast<uint16_t>(e);
+  __syncthreads();
+
+  const uint32_t mid = (W + (W & 1)) / 2 - 1;  // 0-based order statistic of the lower middle
   const bool odd = (W & 1) != 0;
-  for (uint32_t t = threadIdx.x; t < per_block; t += blockDim.x) {
-    const uint32_t o = o0 + t;
-    if (o >= n_out) break;
-    uint32_t cnt = 0;
-    float a = 0.0f, bval = 0.0f;
-    bool have_a = false;
-    for (int e = 0; e < SPAN; ++e) {
-      const uint32_t p = pos[e];
-      if (p >= t && p < t + W) {
-        if (cnt == mid) {
-          a = key[e];
-          have_a = true;
-          if (odd) break;
-        } else if (cnt == mid + 1) {
-          bval = key[e];
-          break;
-        }
-        ++cnt;
-      }
+  const uint32_t run = (per_block + NT - 1) / NT;
+  const uint32_t t0 = threadIdx.x * run;
+  uint32_t t1 = min(t0 + run, per_block);
+  if (o0 + t1 > n_out) t1 = n_out > o0 ? n_out - o0 : 0;
+  if (t0 >= t1) return;
+  auto member = [&](int e, uint32_t t) {
+    const uint32_t p = pos[e];
+    return p >= t && p < t + W;
+  };
+  // first window: scan to the mid-th member
+  int m = 0;
+  uint32_t below = 0;  // members with sorted index < m
+  for (;; ++m) {
+    if (member(m, t0)) {
+      if (below == mid) break;
+      ++below;
     }
-    (void)have_a;
-    med[o] = odd ? a : static_cast<float>(static_cast<double>(a + bval) / 2.0);
+  }
+  for (uint32_t t = t0;; ++t) {
+    // a = key[m]; b = next member's key (even window)
+    float b = 0.0f;
+    if (!odd) {
+      int e = m + 1;
+      while (!member(e, t)) ++e;
+      b = key[e];
+    }
+    const float a = key[m];
+    med[o0 + t] = odd ? a : static_cast<float>(static_cast<double>(a + b) / 2.0);
+    if (t + 1 >= t1) break;
+    // slide: remove position t, insert position t + W
+    const int ro = rank[t], ri = rank[t + W];
+    below = below - (ro < m ? 1u : 0u) + (ri < m ? 1u : 0u);
+    const uint32_t tn = t + 1;
+    // restore: m is a member and exactly `mid` members lie below it
+    while (below > mid) {  // move back to the previous member
+      --m;
+      while (!member(m, tn)) --m;
+      --below;
+    }
+    while (!member(m, tn) || below < mid) {
+      if (member(m, tn)) ++below;
+      ++m;
+      while (!member(m, tn)) ++m;
+    }
   }
 }
 
@@ -132,17 +162,10 @@ bool running_median_supported(uint32_t W) { return W >= 1 && W <= 3072; }
 hipError_t launch_running_median(const float* in, uint32_t n_in, uint32_t W, float* med, hipStream_t s) {
   if (!running_median_supported(W) || n_in < W) return hipErrorInvalidValue;
   const uint32_t n_out = n_in - W + 1;
-  if (W <= 1024) {
-    constexpr int kSpan = 2048;
-    const uint32_t per = kSpan - W + 1;
-    hipLaunchKernelGGL((running_median_kernel<kSpan>), dim3((n_out + per - 1) / per), dim3(1024), 0, s, in, n_in, W,
-                       med, n_out, per);
-  } else {
-    constexpr int kSpan = 4096;
-    const uint32_t per = kSpan - W + 1;
-    hipLaunchKernelGGL((running_median_kernel<kSpan>), dim3((n_out + per - 1) / per), dim3(1024), 0, s, in, n_in, W,
-                       med, n_out, per);
-  }
+  constexpr int kSpan = 4096, kThreads = 256;
+  const uint32_t per = kSpan - W + 1;
+  hipLaunchKernelGGL((running_median_kernel<kSpan, kThreads>), dim3((n_out + per - 1) / per), dim3(kThreads), 0, s, in,
+                     n_in, W, med, n_out, per);
   return hipGetLastError();
 }
 
