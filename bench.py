@@ -102,6 +102,7 @@ def main() -> int:
     table = None
     for _ in range(args.warmup):
         table = search.step(limit)
+    first = bytes(table.to_bytes()) if table is not None else None
     barrier(ctx)
     if torch.cuda.is_available():
         torch.cuda.synchronize()
@@ -140,6 +141,7 @@ def main() -> int:
             "data": data_desc,
             "recall_vs_golden": rec,
             "candidates_in_table": n_cands,
+            "table_identical_to_warmup": (first == bytes(table.to_bytes())) if first is not None else None,
             "gpu_ms_rank0": round(stats["gpu_ms"], 3),
             "whiten_ms_rank0": round(stats["whiten_ms"], 3),
             "phase_ms_per_step_rank0": {k: round(1e3 * v / args.steps, 2) for k, v in search.timings.items()},

@@ -15,6 +15,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <unordered_map>
 
 #include "../core/errors.hpp"
 #include "../core/gsl_compat.hpp"
@@ -412,7 +413,8 @@ int HipEngine::setup(const SearchGeometry& g, const std::vector<float>& series, 
   const size_t B = static_cast<size_t>(d.batch);
   if ((rc = d.series.alloc(g.n_unpadded))) return rc;
   if ((rc = d.buf.alloc(B * d.plan.M))) return rc;
-  if ((rc = d.ps.alloc(B * d.ps_stride))) return rc;
+  // + slack: the harmonic-sum staging copies whole 64-float chunks past the last bin
+  if ((rc = d.ps.alloc(B * d.ps_stride + 1024))) return rc;
   if ((rc = d.partials.alloc(B * d.plan.wg1()))) return rc;
   if ((rc = d.delta.alloc(B))) return rc;
   if (B > hipk::kHsMaxBatch || g.fundamental_idx_hi >= (1u << hipk::kHsBinBits)) {
@@ -524,16 +526,31 @@ int HipEngine::whiten(const SearchOptions& opt, const std::vector<ZapRange>& zap
   DevBuf<uint32_t> zbins;
   DevBuf<float2> znoise;
   const uint32_t nz = static_cast<uint32_t>(noise.bin.size());
+  // host sources of the async copies must outlive them: kept until the final
+  // stream synchronisation of this function
+  std::vector<float2> zn;
+  std::vector<uint32_t> zb;
   if (nz) {
-    std::vector<float2> zn(nz);
-    for (uint32_t i = 0; i < nz; ++i) zn[i] = make_float2(noise.re[i], noise.im[i]);
-    if ((rc = zbins.alloc(nz))) return rc;
-    if ((rc = znoise.alloc(nz))) return rc;
-    BRP_HIP_CHECK(hipMemcpyAsync(zbins.p, noise.bin.data(), nz * sizeof(uint32_t), hipMemcpyHostToDevice, s),
+    // overlapping zap ranges hit a bin more than once: sequentially the last
+    // draw wins, so keep only that one (the device writes bins in parallel)
+    std::unordered_map<uint32_t, uint32_t> last;
+    last.reserve(nz);
+    for (uint32_t i = 0; i < nz; ++i) last[noise.bin[i]] = i;
+    for (uint32_t i = 0; i < nz; ++i) {
+      if (last[noise.bin[i]] != i) continue;
+      zb.push_back(noise.bin[i]);
+      zn.push_back(make_float2(noise.re[i], noise.im[i]));
+    }
+  }
+  const uint32_t nzu = static_cast<uint32_t>(zb.size());
+  if (nzu) {
+    if ((rc = zbins.alloc(nzu))) return rc;
+    if ((rc = znoise.alloc(nzu))) return rc;
+    BRP_HIP_CHECK(hipMemcpyAsync(zbins.p, zb.data(), nzu * sizeof(uint32_t), hipMemcpyHostToDevice, s),
                   RADPUL_HIP_MEM_COPY_HOST_DEVICE);
-    BRP_HIP_CHECK(hipMemcpyAsync(znoise.p, zn.data(), nz * sizeof(float2), hipMemcpyHostToDevice, s),
+    BRP_HIP_CHECK(hipMemcpyAsync(znoise.p, zn.data(), nzu * sizeof(float2), hipMemcpyHostToDevice, s),
                   RADPUL_HIP_MEM_COPY_HOST_DEVICE);
-    BRP_HIP_CHECK(hipk::launch_zap(spec.p, fft_size, zbins.p, znoise.p, nz, s), RADPUL_HIP_KERNEL_INVOKE);
+    BRP_HIP_CHECK(hipk::launch_zap(spec.p, fft_size, zbins.p, znoise.p, nzu, s), RADPUL_HIP_KERNEL_INVOKE);
   }
   // inverse c2r: tangle, conj-FFT, natural order, scale by 1/sqrt(N), keep n_unpadded
   DevBuf<float2>& z = d.w_z;

@@ -106,3 +106,22 @@ def test_running_median_gpu_exact(brp, gpu, tmp_path):
         w_gpu = eng.whiten(opt, [], series)
         rms = float(np.sqrt(np.mean(w_cpu.astype(np.float64) ** 2)))
         assert np.max(np.abs(w_gpu - w_cpu)) / rms < 1e-4, window
+
+
+def test_whitening_overlapping_zaps_deterministic(brp, gpu, tmp_path):
+    """Overlapping zap ranges hit bins several times; the sequential reference
+    keeps the last draw. The device result must match the CPU and be identical
+    run to run (a parallel write of duplicates would race)."""
+    case = synth.synthetic_case(tmp_path, n=1 << 16, n_templates=1)
+    hdr, series, _ = brp.read_work_unit(case["wu"])
+    opt = dict(f0=200.0, padding=3.0, fA=0.08, window=200, white=True)
+    geom = brp.derive_geometry(hdr, opt)
+    zaps = [(10.0, 12.0), (11.0, 13.0), (11.5, 11.6), (50.0, 50.5), (49.9, 50.2)]
+    w_cpu = brp.cpu_whiten(series, geom, opt, zaps)
+    eng = _engine(brp, geom, series)
+    w1 = eng.whiten(opt, zaps, series)
+    eng.setup(geom, np.ascontiguousarray(series, dtype=np.float32), float(np.mean(series)))
+    w2 = eng.whiten(opt, zaps, series)
+    np.testing.assert_array_equal(w1, w2)
+    rms = float(np.sqrt(np.mean(w_cpu.astype(np.float64) ** 2)))
+    assert np.max(np.abs(w1 - w_cpu)) / rms < 1e-4
