@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--streams", type=int, default=int(os.environ.get("BRP_STREAMS", "2")),
                     help="independent pipelines (stream + buffers) per GPU; >1 overlaps host sync with compute")
     ap.add_argument("--templates", type=int, default=0, help="limit the bank (0 = all 6662)")
+    ap.add_argument("--wus", type=int, default=1,
+                    help="work units resident per GPU (config 4): the reference WU + synthetic WUs of its shape")
     ap.add_argument("--synthetic", action="store_true", help="synthetic WU/bank of the benchmark shape")
     ap.add_argument("--write-output", default="", help="rank 0 writes the result file of the last step here")
     return ap.parse_args()
@@ -94,15 +96,29 @@ def main() -> int:
         data_desc = "synthetic: 2^22-sample 4-bit WU with an injected binary pulsar + random 6662-template bank"
     opts = dict(inputfile=str(wu), templatebank=str(bank), zaplistfile=str(zap), f0=400.0, padding=3.0, fA=0.08,
                 window=1000, white=True, batch=args.batch, outputfile=args.write_output)
-    search = ShardedSearch(opts, ctx, streams=args.streams)
+    n_wus = max(1, args.wus)
+    if n_wus > 1:
+        from boinc_app_eah_brp_amd.models import MultiWUSearch, SearchConfig
+        from boinc_app_eah_brp_amd.models.multi import same_shape_synthetic_wus
+
+        hdr, _, _ = brp.read_work_unit(str(wu))
+        extra = same_shape_synthetic_wus(Path(os.environ.get("TMPDIR", "/tmp")) / "brp_bench_wus", hdr, n_wus - 1)
+        cfg = SearchConfig.benchmark(str(wu), str(bank), str(zap), batch=args.batch)
+        search = MultiWUSearch([str(wu)] + extra, cfg, pipelines=args.streams, ctx=ctx)
+        data_desc += f" + {n_wus - 1} synthetic WUs of the same shape (noise + injected binary pulsars)"
+    else:
+        search = ShardedSearch(opts, ctx, streams=args.streams)
     limit = args.templates if args.templates > 0 else search.total
+
+    def first_table(t):
+        return t[0] if isinstance(t, list) else t
     if torch.cuda.is_available():
         torch.cuda.synchronize()
 
     table = None
     for _ in range(args.warmup):
         table = search.step(limit)
-    first = bytes(table.to_bytes()) if table is not None else None
+    first = bytes(first_table(table).to_bytes()) if table is not None else None
     barrier(ctx)
     if torch.cuda.is_available():
         torch.cuda.synchronize()
@@ -115,12 +131,14 @@ def main() -> int:
         torch.cuda.synchronize()
     elapsed = max_over_ranks(time.perf_counter() - t0, ctx)
 
-    if args.write_output:
+    tables = table if isinstance(table, list) else [table]
+    table = tables[0]
+    if args.write_output and n_wus == 1:
         search.write_output(table, limit)
     stats = search.session.stats()
     if ctx.rank == 0:
         geom = search.session.geometry()
-        total = limit * args.steps
+        total = limit * args.steps * n_wus
         value = total / elapsed
         n_cands = sum(1 for e in table.entries() if e[5] > 0)
         rec = recall_vs_golden(table, geom) if limit == search.total else None
@@ -153,6 +171,8 @@ def main() -> int:
                 "fft_len": int(geom["nsamples"]),
                 "parallelism": f"dp{world} (template-bank sharding, RCCL all-gather of candidate tables)",
                 "device_batch": args.batch,
+                "pipelines_per_gpu": args.streams,
+                "work_units": n_wus,
             },
         }
         print(json.dumps(out), flush=True)

@@ -1,0 +1,261 @@
+#include "multi.hpp"
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <thread>
+
+#include "../core/errors.hpp"
+#include "../core/io.hpp"
+#include "../core/log.hpp"
+#include "../engine/hip_engine.hpp"
+
+namespace brp {
+
+namespace {
+
+double now_s() {
+  using namespace std::chrono;
+  return duration<double>(steady_clock::now().time_since_epoch()).count();
+}
+
+bool same_shape(const SearchGeometry& a, const SearchGeometry& b) {
+  return a.nsamples == b.nsamples && a.n_unpadded == b.n_unpadded && a.fft_size == b.fft_size &&
+         a.window_2 == b.window_2 && a.fundamental_idx_hi == b.fundamental_idx_hi &&
+         a.harmonic_idx_hi == b.harmonic_idx_hi && a.dt == b.dt && a.step_inv == b.step_inv;
+}
+
+}  // namespace
+
+struct MultiSession::Impl {
+  SearchOptions opt;
+  SearchControl ctl;
+  TemplateBank bank;
+  std::vector<WorkUnit> wus;
+  std::vector<SearchGeometry> geoms;
+  std::vector<ZapRange> zaps;
+  std::vector<std::unique_ptr<HipEngine>> engines;
+  std::vector<std::string> inputs;
+};
+
+MultiSession::MultiSession() : impl_(new Impl) {}
+MultiSession::~MultiSession() = default;
+size_t MultiSession::work_units() const { return impl_->wus.size(); }
+uint32_t MultiSession::total() const { return static_cast<uint32_t>(impl_->bank.size()); }
+const SearchGeometry& MultiSession::geometry() const { return impl_->geoms.at(0); }
+
+BackendStats MultiSession::stats() const {
+  BackendStats t;
+  for (auto& e : impl_->engines) {
+    const BackendStats s = e->stats();
+    t.gpu_ms += s.gpu_ms;
+    t.whiten_ms += s.whiten_ms;
+    t.templates += s.templates;
+    t.batches += s.batches;
+    t.overflow_reruns += s.overflow_reruns;
+  }
+  return t;
+}
+
+int MultiSession::open(const std::vector<std::string>& inputs, const SearchOptions& opt, const SearchControl& ctl) {
+  Impl& d = *impl_;
+  if (inputs.empty()) return RADPUL_EVAL;
+  d.opt = opt;
+  d.ctl = ctl;
+  d.inputs = inputs;
+  int rc = read_template_bank(opt.templatebank, d.bank);
+  if (rc) return rc;
+  if (opt.white) {
+    if (opt.zaplistfile.empty()) {
+      log_message(LOG_ERROR, true, "Whitening requested but no zaplist file given (-l).\n");
+      return RADPUL_EFILE;
+    }
+    if ((rc = read_zaplist(opt.zaplistfile, d.zaps))) return rc;
+  }
+  d.wus.resize(inputs.size());
+  d.geoms.resize(inputs.size());
+  for (size_t k = 0; k < inputs.size(); ++k) {
+    if ((rc = read_work_unit(inputs[k], d.wus[k]))) return rc;
+    if ((rc = derive_geometry(d.wus[k].header, opt, d.geoms[k]))) return rc;
+    if (!same_shape(d.geoms[k], d.geoms[0])) {
+      log_message(LOG_ERROR, true, "Work unit %s differs in shape from %s; batch only same-shape WUs.\n",
+                  inputs[k].c_str(), inputs[0].c_str());
+      return RADPUL_EVAL;
+    }
+  }
+  if (!hip_backend_supports(d.geoms[0])) {
+    log_message(LOG_ERROR, true, "No HIP FFT plan for N = %u.\n", d.geoms[0].nsamples);
+    return RADPUL_HIP_FFT_PLAN;
+  }
+  const int np = std::max(1, ctl.gpus);
+  for (int e = 0; e < np; ++e) {
+    auto eng = std::make_unique<HipEngine>();
+    int dev = opt.device;
+    if (!ctl.devices.empty()) dev = ctl.devices[e % ctl.devices.size()];
+    else if (np > 1) dev = e;
+    if ((rc = eng->init(dev, opt.batch > 0 ? opt.batch : 8))) return rc;
+    if ((rc = eng->set_slots(static_cast<uint32_t>(inputs.size())))) return rc;
+    d.engines.push_back(std::move(eng));
+  }
+  return 0;
+}
+
+int MultiSession::prepare() {
+  Impl& d = *impl_;
+  const SearchGeometry& g = d.geoms[0];
+  int rc;
+  std::vector<std::vector<float>> prepared(d.wus.size());
+  std::vector<float> mu0(d.wus.size(), 0.0f);
+  HipEngine& e0 = *d.engines[0];
+  for (size_t k = 0; k < d.wus.size(); ++k) {
+    std::vector<float>& s = prepared[k];
+    s = d.wus[k].samples;
+    double mean = 0.0;
+    for (float v : s) mean += v;
+    mean = s.empty() ? 0.0 : mean / s.size();
+    if (k == 0) rc = e0.setup(g, s, static_cast<float>(mean));
+    else rc = e0.load_slot(static_cast<uint32_t>(k), s, static_cast<float>(mean));
+    if (rc) return rc;
+    mu0[k] = static_cast<float>(mean);
+    if (d.opt.white) {
+      // per-WU geometry carries the WU's own t_obs for the zap bins
+      if ((rc = e0.whiten(d.opt, d.zaps, s, static_cast<uint32_t>(k)))) return rc;
+      mu0[k] = 0.0f;
+    }
+  }
+  for (size_t e = 1; e < d.engines.size(); ++e) {
+    for (size_t k = 0; k < d.wus.size(); ++k) {
+      if (k == 0) rc = d.engines[e]->setup(g, prepared[0], mu0[0]);
+      else rc = d.engines[e]->load_slot(static_cast<uint32_t>(k), prepared[k], mu0[k]);
+      if (rc) return rc;
+    }
+  }
+  return 0;
+}
+
+int MultiSession::run(uint32_t begin, uint32_t end, std::vector<CandidateTable>& tables, MultiResult& res) {
+  Impl& d = *impl_;
+  const SearchGeometry& g = d.geoms[0];
+  const uint32_t K = static_cast<uint32_t>(d.wus.size());
+  end = std::min<uint32_t>(end == 0 ? total() : end, total());
+  tables.resize(K);
+  if (begin >= end) return 0;
+  const double t0 = now_s();
+  const uint64_t npairs = static_cast<uint64_t>(end - begin) * K;
+  const int B = d.engines[0]->batch();
+  // device thresholds per WU (lag by the batches in flight; exact ones on the host)
+  std::vector<float> thr_wu(static_cast<size_t>(K) * kNumHarmonicLevels);
+  for (uint32_t w = 0; w < K; ++w) tables[w].thresholds(g.chi2_thr, &thr_wu[w * kNumHarmonicLevels]);
+  struct Batch {
+    uint64_t first = 0;
+    int rc = 0;
+    std::vector<TemplateInput> tin;
+    std::vector<TemplateCands> cands;
+  };
+  std::mutex mu;
+  std::condition_variable cv;
+  std::map<uint64_t, Batch> ready;
+  std::atomic<uint64_t> next{0};
+  std::atomic<bool> stop{false};
+  // deal order: blocks of B templates, WU by WU within a block. A batch then
+  // holds templates of one WU (they share the series in L2), and every WU
+  // still sees its templates in increasing order.
+  std::vector<std::pair<uint32_t, uint32_t>> order;  // (template, WU)
+  order.reserve(npairs);
+  for (uint32_t t0 = begin; t0 < end; t0 += static_cast<uint32_t>(B))
+    for (uint32_t w = 0; w < K; ++w)
+      for (uint32_t t = t0; t < std::min<uint32_t>(t0 + B, end); ++t) order.emplace_back(t, w);
+  auto pair_input = [&](uint64_t q) {
+    const uint32_t t = order[q].first;
+    const uint32_t w = order[q].second;
+    TemplateInput ti{static_cast<float>(d.bank.P[t]), static_cast<float>(d.bank.tau[t]),
+                     static_cast<float>(d.bank.Psi0[t])};
+    ti.wu = w;
+    return ti;
+  };
+  auto worker = [&](HipEngine* eng) {
+    std::vector<float> thr;
+    for (;;) {
+      if (stop.load()) return;
+      const uint64_t first = next.fetch_add(static_cast<uint64_t>(B));
+      if (first >= npairs) return;
+      const int n = static_cast<int>(std::min<uint64_t>(B, npairs - first));
+      Batch bt;
+      bt.first = first;
+      thr.assign(static_cast<size_t>(n) * kNumHarmonicLevels, 0.0f);
+      for (int i = 0; i < n; ++i) bt.tin.push_back(pair_input(first + i));
+      {
+        std::lock_guard<std::mutex> lk(mu);
+        for (int i = 0; i < n; ++i)
+          std::memcpy(&thr[static_cast<size_t>(i) * kNumHarmonicLevels],
+                      &thr_wu[static_cast<size_t>(bt.tin[i].wu) * kNumHarmonicLevels],
+                      sizeof(float) * kNumHarmonicLevels);
+      }
+      bt.rc = eng->process(bt.tin.data(), n, thr.data(), kNumHarmonicLevels, bt.cands);
+      {
+        std::lock_guard<std::mutex> lk(mu);
+        ready.emplace(first, std::move(bt));
+      }
+      cv.notify_all();
+    }
+  };
+  std::vector<std::thread> threads;
+  for (auto& e : d.engines) threads.emplace_back(worker, e.get());
+  uint64_t applied = 0;
+  int rc = 0;
+  while (applied < npairs) {
+    Batch bt;
+    {
+      std::unique_lock<std::mutex> lk(mu);
+      cv.wait(lk, [&] { return ready.count(applied) > 0; });
+      bt = std::move(ready[applied]);
+      ready.erase(applied);
+    }
+    if (bt.rc) {
+      rc = bt.rc;
+      break;
+    }
+    for (size_t i = 0; i < bt.cands.size(); ++i) {
+      const TemplateInput& ti = bt.tin[i];
+      CandidateTable& tab = tables[ti.wu];
+      float thrA[kNumHarmonicLevels];
+      tab.thresholds(d.geoms[ti.wu].chi2_thr, thrA);
+      for (int h = 0; h < kNumHarmonicLevels; ++h) {
+        const std::vector<BinPower>& lv = bt.cands[i].level[h];
+        tab.apply_level(h, lv.data(), lv.size(), thrA[h], ti.P, ti.tau, ti.Psi0);
+      }
+      ++res.pairs_run;
+    }
+    applied = bt.first + bt.cands.size();
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      for (uint32_t w = 0; w < K; ++w) tables[w].thresholds(d.geoms[w].chi2_thr, &thr_wu[w * kNumHarmonicLevels]);
+    }
+  }
+  stop.store(true);
+  for (auto& th : threads) th.join();
+  res.t_templates += now_s() - t0;
+  res.stats = stats();
+  return rc;
+}
+
+int MultiSession::finalize(const std::vector<std::string>& outputs, uint32_t n_done,
+                           std::vector<CandidateTable>& tables) {
+  Impl& d = *impl_;
+  if (outputs.size() != d.wus.size() || tables.size() != d.wus.size()) return RADPUL_EVAL;
+  for (size_t k = 0; k < d.wus.size(); ++k) {
+    SearchOptions o = d.opt;
+    o.inputfile = d.inputs[k];
+    o.outputfile = outputs[k];
+    if (!o.checkpointfile.empty()) o.checkpointfile = d.opt.checkpointfile + "." + std::to_string(k);
+    const int rc = finalize_output(o, d.geoms[k], n_done, tables[k], "einsteinbinary_mi355x");
+    if (rc) return rc;
+  }
+  return 0;
+}
+
+}  // namespace brp

@@ -7,6 +7,7 @@
 #include <cstring>
 #include <stdexcept>
 
+#include "../app/multi.hpp"
 #include "../app/search.hpp"
 #include "../boinc/boinc_shim.hpp"
 #include "../boinc/ipc.hpp"
@@ -529,6 +530,60 @@ PYBIND11_MODULE(_brp, m) {
         d["templates"] = st.templates;
         d["batches"] = st.batches;
         d["overflow_reruns"] = st.overflow_reruns;
+        return d;
+      });
+  py::class_<MultiSession>(m, "MultiSession")
+      .def(py::init<>())
+      .def(
+          "open",
+          [](MultiSession& s, std::vector<std::string> inputs, const py::dict& od, int pipelines,
+             std::vector<int> devices) {
+            SearchControl ctl;
+            ctl.gpus = pipelines;
+            ctl.devices = devices;
+            check(s.open(inputs, dict_to_options(od), ctl), "MultiSession.open");
+          },
+          py::arg("inputs"), py::arg("options"), py::arg("pipelines") = 1, py::arg("devices") = std::vector<int>())
+      .def("prepare",
+           [](MultiSession& s) {
+             int rc;
+             {
+               py::gil_scoped_release rel;
+               rc = s.prepare();
+             }
+             check(rc, "MultiSession.prepare");
+           })
+      .def(
+          "run",
+          [](MultiSession& s, uint32_t begin, uint32_t end) {
+            std::vector<CandidateTable> tables;
+            MultiResult res;
+            int rc;
+            {
+              py::gil_scoped_release rel;
+              rc = s.run(begin, end, tables, res);
+            }
+            check(rc, "MultiSession.run");
+            py::dict d;
+            d["pairs_run"] = res.pairs_run;
+            d["t_templates"] = res.t_templates;
+            return py::make_tuple(tables, d);
+          },
+          py::arg("begin") = 0, py::arg("end") = 0)
+      .def("finalize",
+           [](MultiSession& s, std::vector<std::string> outputs, uint32_t n_done, std::vector<CandidateTable> tables) {
+             check(s.finalize(outputs, n_done, tables), "MultiSession.finalize");
+           })
+      .def("work_units", &MultiSession::work_units)
+      .def("total", &MultiSession::total)
+      .def("geometry", [](MultiSession& s) { return geometry_to_dict(s.geometry()); })
+      .def("stats", [](MultiSession& s) {
+        const BackendStats st = s.stats();
+        py::dict d;
+        d["gpu_ms"] = st.gpu_ms;
+        d["whiten_ms"] = st.whiten_ms;
+        d["templates"] = st.templates;
+        d["batches"] = st.batches;
         return d;
       });
   m.def("finalize_output", [](const py::dict& od, const py::dict& gd, uint32_t n_done, CandidateTable t) {

@@ -16,6 +16,7 @@ namespace brp {
 
 struct TemplateInput {
   float P, tau, Psi0;
+  uint32_t wu = 0;  // work-unit slot (multi-WU batching)
 };
 
 struct TemplateCands {

@@ -154,7 +154,6 @@ struct HipEngine::Impl {
   SearchGeometry g;
   FFTPlan3 plan;
   bool ready = false;
-  float mu0 = 0.0f;
   uint32_t p3_exp = 0;          // BRP_P3_EXP profiling switches (pass3_kernel)
   uint32_t num_cus = 256;
   uint32_t persist_per_cu = 4;  // persistent FFT passes: workgroups per CU (BRP_PERSIST, 0 = off)
@@ -180,7 +179,9 @@ struct HipEngine::Impl {
   struct { TemplateDev* p = nullptr; } h_tmpl;
   struct { float* p = nullptr; } h_thr;
   PinnedBuf<uint2> h_cands;     // [1 + kcopy]
-  static constexpr size_t kThrBytes = 64;  // thresholds area at the start of `in`
+  size_t thr_bytes = 64;        // thresholds area at the start of `in`: [batch][kHsThrStride] floats
+  uint32_t slots = 1;           // work-unit slots of the series buffer (multi-WU batching)
+  std::vector<float> mu0s;      // per-slot padding offset
 
   std::map<int, hipGraphExec_t> graphs;
   BackendStats st;
@@ -256,7 +257,7 @@ struct HipEngine::Impl {
     const hipk::TwiddleTable tw = twt();
     switch (st) {
       case kPrologue:
-        e = hipMemcpyAsync(in.p, h_in.p, kThrBytes + sizeof(TemplateDev) * nb, hipMemcpyHostToDevice, stream);
+        e = hipMemcpyAsync(in.p, h_in.p, thr_bytes + sizeof(TemplateDev) * nb, hipMemcpyHostToDevice, stream);
         if (e != hipSuccess) return e;
         return hipk::launch_nsteps(tmpl.p, nb, stream, &cands.p[0].x);
       case kPass1: {
@@ -386,7 +387,8 @@ int HipEngine::setup(const SearchGeometry& g, const std::vector<float>& series, 
     // next work unit of the same shape (or the same WU again): buffers, tables
     // and captured graphs stay valid; only the series and its mean change
     d.g = g;
-    d.mu0 = mu0;
+    d.mu0s.assign(d.slots, 0.0f);
+    d.mu0s[0] = mu0;
     BRP_HIP_CHECK(hipMemcpy(d.series.p, series.data(), g.n_unpadded * sizeof(float), hipMemcpyHostToDevice),
                   RADPUL_HIP_MEM_COPY_HOST_DEVICE);
     return 0;
@@ -395,7 +397,8 @@ int HipEngine::setup(const SearchGeometry& g, const std::vector<float>& series, 
   for (auto& kv : d.graphs) (void)hipGraphExecDestroy(kv.second);
   d.graphs.clear();
   d.g = g;
-  d.mu0 = mu0;
+  d.mu0s.assign(d.slots, 0.0f);
+  d.mu0s[0] = mu0;
   if (g.nsamples % 2 || !make_fft_plan(g.nsamples / 2, d.plan)) {
     log_message(LOG_ERROR, true, "Unsupported FFT length %u (need N/2 = L1*L2*L3 from the compiled set).\n",
                 g.nsamples);
@@ -411,7 +414,7 @@ int HipEngine::setup(const SearchGeometry& g, const std::vector<float>& series, 
   if (d.i_start > g.window_2) d.i_start = 8;  // unreachable; keeps the invariant i_start <= w2 for w2 >= 8
   int rc;
   const size_t B = static_cast<size_t>(d.batch);
-  if ((rc = d.series.alloc(g.n_unpadded))) return rc;
+  if ((rc = d.series.alloc(static_cast<size_t>(d.slots) * g.n_unpadded))) return rc;
   if ((rc = d.buf.alloc(B * d.plan.M))) return rc;
   // + slack: the harmonic-sum staging copies whole 64-float chunks past the last bin
   if ((rc = d.ps.alloc(B * d.ps_stride + 1024))) return rc;
@@ -422,14 +425,15 @@ int HipEngine::setup(const SearchGeometry& g, const std::vector<float>& series, 
                 g.fundamental_idx_hi);
     return RADPUL_EVAL;
   }
-  const size_t in_bytes = Impl::kThrBytes + sizeof(TemplateDev) * B;
+  d.thr_bytes = (B * hipk::kHsThrStride * sizeof(float) + 63) / 64 * 64;
+  const size_t in_bytes = d.thr_bytes + sizeof(TemplateDev) * B;
   if ((rc = d.in.alloc(in_bytes))) return rc;
   d.thr.p = reinterpret_cast<float*>(d.in.p);
-  d.tmpl.p = reinterpret_cast<TemplateDev*>(d.in.p + Impl::kThrBytes);
+  d.tmpl.p = reinterpret_cast<TemplateDev*>(d.in.p + d.thr_bytes);
   if ((rc = d.cands.alloc(1 + d.cap))) return rc;
   if ((rc = d.h_in.alloc(in_bytes))) return rc;
   d.h_thr.p = reinterpret_cast<float*>(d.h_in.p);
-  d.h_tmpl.p = reinterpret_cast<TemplateDev*>(d.h_in.p + Impl::kThrBytes);
+  d.h_tmpl.p = reinterpret_cast<TemplateDev*>(d.h_in.p + d.thr_bytes);
   if ((rc = d.h_cands.alloc(1 + d.kcopy))) return rc;
   std::vector<float2> hi, lo;
   build_twiddles(4ull * d.plan.M, hi, lo);
@@ -446,16 +450,36 @@ int HipEngine::setup(const SearchGeometry& g, const std::vector<float>& series, 
   return 0;
 }
 
-int HipEngine::upload_series(const std::vector<float>& series, float mu0) {
+int HipEngine::upload_series(const std::vector<float>& series, float mu0) { return load_slot(0, series, mu0); }
+
+int HipEngine::set_slots(uint32_t k) {
   Impl& d = *impl_;
-  d.mu0 = mu0;
-  BRP_HIP_CHECK(hipMemcpy(d.series.p, series.data(), d.g.n_unpadded * sizeof(float), hipMemcpyHostToDevice),
+  if (k == 0 || k > (1u << 16)) return RADPUL_EVAL;
+  if (k != d.slots) {
+    d.slots = k;
+    d.ready = false;  // the next setup() reallocates the series buffer
+  }
+  return 0;
+}
+
+uint32_t HipEngine::slots() const { return impl_->slots; }
+
+int HipEngine::load_slot(uint32_t k, const std::vector<float>& series, float mu0) {
+  Impl& d = *impl_;
+  if (!d.ready || k >= d.slots || series.size() < d.g.n_unpadded) return RADPUL_EVAL;
+  BRP_HIP_CHECK(hipSetDevice(d.device), RADPUL_HIP_DEVICE_SET);
+  d.mu0s[k] = mu0;
+  BRP_HIP_CHECK(hipMemcpy(d.series.p + static_cast<size_t>(k) * d.g.n_unpadded, series.data(),
+                          d.g.n_unpadded * sizeof(float), hipMemcpyHostToDevice),
                 RADPUL_HIP_MEM_COPY_HOST_DEVICE);
   return 0;
 }
 
-int HipEngine::whiten(const SearchOptions& opt, const std::vector<ZapRange>& zaps, std::vector<float>& series) {
+int HipEngine::whiten(const SearchOptions& opt, const std::vector<ZapRange>& zaps, std::vector<float>& series,
+                      uint32_t slot) {
   Impl& d = *impl_;
+  if (slot >= d.slots) return RADPUL_EVAL;
+  float* slot_series = d.series.p + static_cast<size_t>(slot) * d.g.n_unpadded;
   const SearchGeometry& g = d.g;
   auto t0 = std::chrono::steady_clock::now();
   int32_t seed;
@@ -482,7 +506,7 @@ int HipEngine::whiten(const SearchOptions& opt, const std::vector<ZapRange>& zap
   a1.L3 = d.plan.L3;
   a1.tw = tw;
   a1.tb = d.tables();
-  a1.real_in = d.series.p;
+  a1.real_in = slot_series;
   a1.n_real = g.n_unpadded;
   BRP_HIP_CHECK(hipk::launch_pass1(d.plan, hipk::P1_REAL, a1, 1, s), RADPUL_HIP_KERNEL_INVOKE);
   hipk::Pass2Args a2{};
@@ -574,18 +598,23 @@ int HipEngine::whiten(const SearchOptions& opt, const std::vector<ZapRange>& zap
   ap.tw = tw;
   ap.tb = d.tables();
   ap.scale = static_cast<float>(1.0 / std::sqrt(static_cast<float>(g.nsamples)));
-  ap.real_out = d.series.p;
+  ap.real_out = slot_series;
   ap.n_out = g.n_unpadded;
   BRP_HIP_CHECK(hipk::launch_pass3_plain(d.plan, ap, s), RADPUL_HIP_KERNEL_INVOKE);
-  BRP_HIP_CHECK(hipMemcpyAsync(series.data(), d.series.p, g.n_unpadded * sizeof(float), hipMemcpyDeviceToHost, s),
+  BRP_HIP_CHECK(hipMemcpyAsync(series.data(), slot_series, g.n_unpadded * sizeof(float), hipMemcpyDeviceToHost, s),
                 RADPUL_HIP_MEM_COPY_DEVICE_HOST);
   BRP_HIP_CHECK(hipStreamSynchronize(s), RADPUL_HIP_KERNEL_INVOKE);
-  d.mu0 = 0.0f;  // whitened series has its DC (and first window_2 bins) removed
+  d.mu0s[slot] = 0.0f;  // whitened series has its DC (and first window_2 bins) removed
   d.st.whiten_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return 0;
 }
 
 int HipEngine::process(const TemplateInput* t, int n, const float thr[kNumHarmonicLevels],
+                       std::vector<TemplateCands>& out) {
+  return process(t, n, thr, 0, out);
+}
+
+int HipEngine::process(const TemplateInput* t, int n, const float* thr, int thr_stride,
                        std::vector<TemplateCands>& out) {
   Impl& d = *impl_;
   if (!d.ready) return RADPUL_EMISC;
@@ -600,10 +629,13 @@ int HipEngine::process(const TemplateInput* t, int n, const float thr[kNumHarmon
       td.p = make_resamp_params(g.nsamples, g.n_unpadded, g.fft_size, g.dt, g.step_inv, t[off + k].P,
                                 t[off + k].tau, t[off + k].Psi0);
       td.n_steps = 0;
-      td.mu0 = d.mu0;
+      if (t[off + k].wu >= d.slots) return RADPUL_EVAL;
+      td.wu = t[off + k].wu;
+      td.mu0 = d.mu0s[td.wu];
       d.h_tmpl.p[k] = td;
+      const float* th = thr + static_cast<size_t>(off + k) * thr_stride;
+      for (int h = 0; h < kNumHarmonicLevels; ++h) d.h_thr.p[k * hipk::kHsThrStride + h] = th[h];
     }
-    std::memcpy(d.h_thr.p, thr, sizeof(float) * kNumHarmonicLevels);
     hipGraphExec_t exec = nullptr;
     auto it = d.graphs.find(nb);
     const bool use_graph = std::getenv("BRP_NO_GRAPH") == nullptr;
@@ -678,7 +710,7 @@ int HipEngine::power_spectrum(const TemplateInput& t, std::vector<float>& ps_out
   const SearchGeometry& g = d.g;
   TemplateDev td{};
   td.p = make_resamp_params(g.nsamples, g.n_unpadded, g.fft_size, g.dt, g.step_inv, t.P, t.tau, t.Psi0);
-  td.mu0 = d.mu0;
+  td.mu0 = d.mu0s[0];
   d.h_tmpl.p[0] = td;
   hipStream_t s = d.stream;
   BRP_HIP_CHECK(hipMemcpyAsync(d.tmpl.p, d.h_tmpl.p, sizeof(TemplateDev), hipMemcpyHostToDevice, s),
@@ -745,10 +777,10 @@ int HipEngine::benchmark_stages(const TemplateInput* t, int n, int reps, std::ve
   for (int k = 0; k < nb; ++k) {
     TemplateDev td{};
     td.p = make_resamp_params(g.nsamples, g.n_unpadded, g.fft_size, g.dt, g.step_inv, t[k].P, t[k].tau, t[k].Psi0);
-    td.mu0 = d.mu0;
+    td.mu0 = d.mu0s[0];
     d.h_tmpl.p[k] = td;
+    for (int h = 0; h < kNumHarmonicLevels; ++h) d.h_thr.p[k * hipk::kHsThrStride + h] = d.g.chi2_thr[h];
   }
-  for (int h = 0; h < kNumHarmonicLevels; ++h) d.h_thr.p[h] = d.g.chi2_thr[h];
   BRP_HIP_CHECK(d.enqueue(nb), RADPUL_HIP_KERNEL_INVOKE);
   BRP_HIP_CHECK(hipStreamSynchronize(d.stream), RADPUL_HIP_KERNEL_INVOKE);
   us_per_launch.assign(Impl::kNumStages + 1, 0.0);

@@ -22,9 +22,19 @@ class HipEngine {
   // subtracted before the FFT (keeps the padding correction well conditioned)
   int setup(const SearchGeometry& g, const std::vector<float>& series, float mu0);
   int upload_series(const std::vector<float>& series, float mu0);
-  // whitening + zapping on the device; `series` receives the whitened data
-  int whiten(const SearchOptions& opt, const std::vector<ZapRange>& zaps, std::vector<float>& series);
+  // Multi-WU batching: the series buffer holds `k` work units of the same
+  // shape (set before setup(); setup() fills slot 0, load_slot() the others).
+  // Templates pick their slot with TemplateInput::wu.
+  int set_slots(uint32_t k);
+  uint32_t slots() const;
+  int load_slot(uint32_t k, const std::vector<float>& series, float mu0);
+  // whitening + zapping of one slot on the device; `series` (that slot's raw
+  // data) receives the whitened data
+  int whiten(const SearchOptions& opt, const std::vector<ZapRange>& zaps, std::vector<float>& series,
+             uint32_t slot = 0);
   int process(const TemplateInput* t, int n, const float thr[kNumHarmonicLevels], std::vector<TemplateCands>& out);
+  // per-template thresholds thr[i * thr_stride + h] (thr_stride 0: shared)
+  int process(const TemplateInput* t, int n, const float* thr, int thr_stride, std::vector<TemplateCands>& out);
   // test hooks
   int power_spectrum(const TemplateInput& t, std::vector<float>& ps, uint32_t* n_steps);
   // time each pipeline stage (prologue, pass1, pass2, pass3, harmonic, epilogue,

@@ -18,7 +18,8 @@ struct TemplateDev {
   ResampParams p;
   uint32_t n_steps;   // samples taken from the series (rest is mean padding)
   float mu0;          // reference level subtracted before the FFT
-  uint32_t pad[2];
+  uint32_t wu;        // work-unit slot: series = Pass1Args::series + wu * n_unpadded
+  uint32_t pad;
 };
 
 // Twiddle tables precomputed on the host per FFT plan (single rounding from
@@ -47,7 +48,7 @@ struct Pass1Args {
   TwiddleTable tw;
   FFTTables tb;
   // P1_RESAMPLE
-  const float* series;         // n_unpadded samples (shared by the batch)
+  const float* series;         // [slots][n_unpadded] samples (slot per template: TemplateDev::wu)
   uint32_t n_unpadded;
   const TemplateDev* tmpl;     // [batch]
   double* partials;            // [batch][wg1] sums of (sample - mu0)

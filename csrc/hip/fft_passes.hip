@@ -86,11 +86,12 @@ __global__ void __launch_bounds__(kNcol * tpc_for<L>()) pass1_kernel(Pass1Args a
     __syncthreads();
     const bool fast = a.n_unpadded <= (1u << 23);
     const TemplateDev td = a.tmpl[b];
+    const float* series = a.series + static_cast<size_t>(td.wu) * a.n_unpadded;
 #pragma unroll 4
     for (int r = tj; r < L; r += TPC) {
       const uint32_t n = r * a.L2L3 + col_base + c;
-      const float x0 = resample_sample(2 * n, td, a.series, a.n_unpadded, lut_s, lut_c, fast);
-      const float x1 = resample_sample(2 * n + 1, td, a.series, a.n_unpadded, lut_s, lut_c, fast);
+      const float x0 = resample_sample(2 * n, td, series, a.n_unpadded, lut_s, lut_c, fast);
+      const float x1 = resample_sample(2 * n + 1, td, series, a.n_unpadded, lut_s, lut_c, fast);
       sum += static_cast<double>(x0) + static_cast<double>(x1);
       data[Lay::idx(r, c)] = make_float2(x0, x1);
     }

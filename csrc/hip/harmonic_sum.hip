@@ -76,7 +76,7 @@ __global__ void __launch_bounds__(kThreads) harmonic_sum_kernel(HSArgs a) {
 
   uint32_t* count = &a.list[0].x;
   uint2* list = a.list + 1;
-  const float thr0 = a.thr[0];
+  const float thr0 = a.thr[static_cast<size_t>(b) * kHsThrStride + 0];
   // level 0: the power spectrum itself
   for (int t = threadIdx.x; t < kHsTile; t += kThreads) {
     const uint32_t i = i0 + t;
@@ -91,7 +91,7 @@ __global__ void __launch_bounds__(kThreads) harmonic_sum_kernel(HSArgs a) {
   for (int h = 1; h <= 4; ++h) {
     const int g = 1 << h;
     const int off = g >> 1;
-    const float thr = a.thr[h];
+    const float thr = a.thr[static_cast<size_t>(b) * kHsThrStride + h];
     const int first = static_cast<int>((off - (i0 % g) + g) % g);
     const int ngroups = (kHsTile - first + g - 1) / g;
     for (int q = threadIdx.x; q < ((ngroups + kThreads - 1) / kThreads) * kThreads; q += kThreads) {

@@ -15,13 +15,14 @@ struct HSArgs {
   uint32_t ps_stride;
   uint32_t w2, fhi, hhi;  // window_2, fundamental_idx_hi, harmonic_idx_hi
   uint32_t i_start;       // first i of tile 0 (== 8 mod 16, <= w2)
-  const float* thr;       // [5] device thresholds for the whole batch
+  const float* thr;       // [batch][kHsThrStride] device thresholds per template
   // one compact list per batch: list[0].x = number of entries (atomic; may
   // exceed cap), list[1 + q] = (hs_pack(template, level, bin), power bits)
   uint2* list;
   uint32_t cap;
 };
 
+constexpr uint32_t kHsThrStride = 8;  // floats per template in the threshold array (5 used)
 constexpr uint32_t kHsBinBits = 23;  // bins < 2^23, levels < 8, templates per batch < 64
 constexpr uint32_t kHsMaxBatch = 64;
 __host__ __device__ constexpr uint32_t hs_pack(uint32_t k, uint32_t h, uint32_t bin) {

@@ -135,3 +135,30 @@ def test_app_binary_gpu(brp, gpu, case, tmp_path):
     rc = BRPSearch(_cfg(case, tmp_path / "c", use_cpu=True)).run()
     lc, _ = brp.read_results(str(tmp_path / "c" / "out.cand"))
     assert lines[0][0] == pytest.approx(lc[0][0], rel=1e-9)
+
+
+def test_multi_wu_batching_matches_single_runs(brp, gpu, tmp_path):
+    """K same-shape WUs resident together, templates of different WUs mixed in
+    every batch: each WU's table equals its own single-WU run byte for byte."""
+    from boinc_app_eah_brp_amd.models import MultiWUSearch
+
+    wus = []
+    for k in range(3):
+        inj = synth.Injection(f0=150.0 + 40 * k, P_orb=900.0 + 100 * k, tau=0.02, psi0=0.5 * k, amplitude=3.0)
+        c = synth.synthetic_case(tmp_path / f"w{k}", n=1 << 16, n_templates=21, inj=inj, seed=10 + k)
+        wus.append(c)
+    bank = wus[0]["bank"]
+    cfg = SearchConfig(inputfile=wus[0]["wu"], templatebank=bank, zaplistfile=wus[0]["zap"], f0=400.0, padding=3.0,
+                       fA=0.08, window=100, white=True, batch=4)
+    ms = MultiWUSearch([c["wu"] for c in wus], cfg, pipelines=2)
+    tables = ms.step()
+    assert len(tables) == 3
+    for k, c in enumerate(wus):
+        single = BRPSearch(_cfg(c, tmp_path / f"s{k}", templatebank=bank, batch=4)).run(write_output=False,
+                                                                                      use_checkpoint=False)
+        assert bytes(tables[k].to_bytes()) == bytes(single.table.to_bytes()), k
+    outs = [str(tmp_path / f"o{k}.cand") for k in range(3)]
+    ms.write_outputs(outs, tables)
+    for o in outs:
+        lines, done = brp.read_results(o)
+        assert done and lines
