@@ -59,21 +59,56 @@ def synthetic_inputs(workdir: Path):
     return Path(case["wu"]), Path(case["bank"]), Path(case["zap"])
 
 
-def recall_vs_golden(table, geom) -> float | None:
-    """Fraction of golden (f0 bin, n_harm) candidates present in this run's output."""
+GOLDEN_TABLE = ROOT / "data" / "golden" / "bench_wu_cpu_table.bin"
+
+
+def recall_vs_golden(table, geom) -> dict | None:
+    """Candidate recall against the CPU golden model run of the whole bank
+    (tools/make_golden.py):
+      results: fraction of the golden result-file lines (top <= 100 by
+               significance, one per frequency) whose (f0 bin, n_harm) appears
+               among this run's result lines;
+      table:   fraction of the golden 5x100 table entries (level, bin) present
+               in this run's table."""
     if not GOLDEN.exists():
         return None
-    golden = set()
-    with open(GOLDEN) as fh:
-        for line in fh:
-            if line.startswith("%") or not line.strip():
-                continue
-            f = line.split()
-            golden.add((round(float(f[0]) * geom["t_obs_d"]), int(f[6])))
-    if not golden:
-        return None
-    ours = {(int(e[0]), int(e[5])) for e in table.entries() if e[5] > 0}
-    return len(golden & ours) / len(golden)
+    import tempfile
+
+    from boinc_app_eah_brp_amd import native
+
+    brp = native()
+    t_obs = geom["t_obs_d"]
+
+    def lines_of(path):
+        out = set()
+        with open(path) as fh:
+            for line in fh:
+                if line.startswith("%") or not line.strip():
+                    continue
+                f = line.split()
+                out.add((round(float(f[0]) * t_obs), int(f[6])))
+        return out
+
+    golden = lines_of(GOLDEN)
+    with tempfile.TemporaryDirectory() as d:
+        p = Path(d) / "ours.cand"
+        brp.write_results(str(p), table, t_obs, False)
+        ours = lines_of(p)
+    rec = {"results": round(len(golden & ours) / max(1, len(golden)), 4), "golden_lines": len(golden)}
+    if GOLDEN_TABLE.exists():
+        import numpy as np
+
+        gt = brp.CandidateTable()
+        gt.from_bytes(np.frombuffer(GOLDEN_TABLE.read_bytes(), dtype=np.uint8).copy())
+
+        def keyset(t):
+            ent = t.entries()
+            return {(k // 100, int(e[0])) for k, e in enumerate(ent) if e[5] > 0}
+
+        g, o = keyset(gt), keyset(table)
+        rec["table"] = round(len(g & o) / max(1, len(g)), 4)
+        rec["golden_entries"] = len(g)
+    return rec
 
 
 def main() -> int:
