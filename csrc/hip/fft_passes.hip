@@ -42,17 +42,6 @@ __device__ __forceinline__ double block_sum(double v, double* scratch) {
 }
 
 
-// One resampled sample (0 beyond n_steps). `lut` = LDS copy of the sine/cosine
-// tables; `fast` selects the float nearest-index path (n_unpadded <= 2^23).
-__device__ __forceinline__ float resample_sample(uint32_t m, const TemplateDev& td, const float* series,
-                                                 uint32_t n_unpadded, const float* lut_s, const float* lut_c,
-                                                 bool fast) {
-  if (m >= td.n_steps) return 0.0f;
-  const float dt = resamp_del_t(m, td.p, lut_s, lut_c);
-  int idx = fast ? resamp_nearest_f(m, dt) : resamp_nearest(m, dt);
-  idx = idx < 0 ? 0 : (idx >= static_cast<int>(n_unpadded) ? static_cast<int>(n_unpadded) - 1 : idx);
-  return series[idx] - td.mu0;
-}
 
 // ------------------------------------------------------------------ pass 1
 template <int L, int MODE>
@@ -87,13 +76,35 @@ __global__ void __launch_bounds__(kNcol * tpc_for<L>()) pass1_kernel(Pass1Args a
     const bool fast = a.n_unpadded <= (1u << 23);
     const TemplateDev td = a.tmpl[b];
     const float* series = a.series + static_cast<size_t>(td.wu) * a.n_unpadded;
-#pragma unroll 4
-    for (int r = tj; r < L; r += TPC) {
-      const uint32_t n = r * a.L2L3 + col_base + c;
-      const float x0 = resample_sample(2 * n, td, series, a.n_unpadded, lut_s, lut_c, fast);
-      const float x1 = resample_sample(2 * n + 1, td, series, a.n_unpadded, lut_s, lut_c, fast);
+    // three phases so that all gathers of the thread are in flight together:
+    // nearest indices (LUT sine, VALU), unconditional clamped loads, then
+    // select/centre/accumulate into LDS
+    constexpr int kPer = L / TPC;
+    const int last = static_cast<int>(a.n_unpadded) - 1;
+    int idx[2 * kPer];
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const uint32_t m0 = 2 * ((tj + u * TPC) * a.L2L3 + col_base + c);
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const uint32_t m = m0 + q;
+        int i = -1;
+        if (m < td.n_steps) {
+          const float dt = resamp_del_t(m, td.p, lut_s, lut_c);
+          i = min(max(fast ? resamp_nearest_f(m, dt) : resamp_nearest(m, dt), 0), last);
+        }
+        idx[2 * u + q] = i;
+      }
+    }
+    float raw[2 * kPer];
+#pragma unroll
+    for (int e = 0; e < 2 * kPer; ++e) raw[e] = series[idx[e] < 0 ? 0 : idx[e]];
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const float x0 = idx[2 * u] < 0 ? 0.0f : raw[2 * u] - td.mu0;
+      const float x1 = idx[2 * u + 1] < 0 ? 0.0f : raw[2 * u + 1] - td.mu0;
       sum += static_cast<double>(x0) + static_cast<double>(x1);
-      data[Lay::idx(r, c)] = make_float2(x0, x1);
+      data[Lay::idx(tj + u * TPC, c)] = make_float2(x0, x1);
     }
   } else if (MODE == P1_REAL) {
     for (int r = tj; r < L; r += TPC) {
