@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--streams", type=int, default=int(os.environ.get("BRP_STREAMS", "2")),
                     help="independent pipelines (stream + buffers) per GPU; >1 overlaps host sync with compute")
     ap.add_argument("--templates", type=int, default=0, help="limit the bank (0 = all 6662)")
+    ap.add_argument("--ps-fp16", action="store_true",
+                    help="config 5: fp16 power spectrum (precision/throughput trade; recall is reported)")
     ap.add_argument("--wus", type=int, default=1,
                     help="work units resident per GPU (config 4): the reference WU + synthetic WUs of its shape")
     ap.add_argument("--synthetic", action="store_true", help="synthetic WU/bank of the benchmark shape")
@@ -130,7 +132,7 @@ def main() -> int:
         wu, bank, zap = synthetic_inputs(Path(os.environ.get("TMPDIR", "/tmp")) / f"brp_bench_{ctx.rank}")
         data_desc = "synthetic: 2^22-sample 4-bit WU with an injected binary pulsar + random 6662-template bank"
     opts = dict(inputfile=str(wu), templatebank=str(bank), zaplistfile=str(zap), f0=400.0, padding=3.0, fA=0.08,
-                window=1000, white=True, batch=args.batch, outputfile=args.write_output)
+                window=1000, white=True, batch=args.batch, outputfile=args.write_output, ps_fp16=args.ps_fp16)
     n_wus = max(1, args.wus)
     if n_wus > 1:
         from boinc_app_eah_brp_amd.models import MultiWUSearch, SearchConfig
@@ -138,7 +140,7 @@ def main() -> int:
 
         hdr, _, _ = brp.read_work_unit(str(wu))
         extra = same_shape_synthetic_wus(Path(os.environ.get("TMPDIR", "/tmp")) / "brp_bench_wus", hdr, n_wus - 1)
-        cfg = SearchConfig.benchmark(str(wu), str(bank), str(zap), batch=args.batch)
+        cfg = SearchConfig.benchmark(str(wu), str(bank), str(zap), batch=args.batch, ps_fp16=args.ps_fp16)
         search = MultiWUSearch([str(wu)] + extra, cfg, pipelines=args.streams, ctx=ctx)
         data_desc += f" + {n_wus - 1} synthetic WUs of the same shape (noise + injected binary pulsars)"
     else:
@@ -190,7 +192,7 @@ def main() -> int:
             "vs_baseline": None,
             "baseline_note": "reference publishes no templates/s; BASELINE.md derives ~2.1 templates/s per CPU core",
             "vs_derived_cpu_core": round(value / 2.1, 1),
-            "dtype": "fp32",
+            "dtype": "fp32 (fp16 power spectrum)" if args.ps_fp16 else "fp32",
             "data": data_desc,
             "recall_vs_golden": rec,
             "candidates_in_table": n_cands,

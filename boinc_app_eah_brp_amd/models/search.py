@@ -30,6 +30,7 @@ class SearchConfig:
     device: int = -1         # -D
     batch: int = 4           # templates per device batch
     use_cpu: bool = False
+    ps_fp16: bool = False    # fp16 power spectrum (config 5 precision/throughput trade; needs white)
 
     @classmethod
     def benchmark(cls, wu: str, bank: str, zap: str, **kw) -> "SearchConfig":

@@ -41,6 +41,7 @@ void print_usage(const char* prog) {
   std::printf(" --mi355x-batch\t\tinteger\tTemplates per device batch (default 4).\n");
   std::printf(" --mi355x-gpus\t\tinteger\tGPUs (or CPU worker threads with --mi355x-cpu) driven by this process (default 1).\n");
   std::printf(" --mi355x-cpu\t\t\tboolean\tUse the CPU golden backend.\n");
+  std::printf(" --mi355x-ps-fp16\t\tboolean\tStore the power spectrum as fp16 (needs -W).\n");
   std::printf("\n");
 }
 
@@ -166,6 +167,8 @@ int search_main(int argc, char** argv) {
       if (!v) return RADPUL_EVAL;
       ctl.gpus = std::max(1, std::atoi(v));
       i += 2;
+    } else if (std::strcmp(a, "--mi355x-ps-fp16") == 0) {
+      opt.ps_fp16 = true;
     } else if (std::strcmp(a, "--mi355x-cpu") == 0) {
       opt.use_cpu = true;
       i++;
@@ -210,6 +213,7 @@ int wrapper_main(int argc, char** argv) {
                                          {"mi355x-batch", required_argument, 0, 1001},
                                          {"mi355x-gpus", required_argument, 0, 1002},
                                          {"mi355x-cpu", no_argument, 0, 1003},
+                                         {"mi355x-ps-fp16", no_argument, 0, 1004},
                                          {0, 0, 0, 0}};
   optind = 1;
   auto file_arg = [&](const char* opt, const char* val) {
@@ -248,6 +252,7 @@ int wrapper_main(int argc, char** argv) {
       case 1001: fwd.push_back("--mi355x-batch"); fwd.push_back(optarg); break;
       case 1002: fwd.push_back("--mi355x-gpus"); fwd.push_back(optarg); break;
       case 1003: fwd.push_back("--mi355x-cpu"); break;
+      case 1004: fwd.push_back("--mi355x-ps-fp16"); break;
       default: boinc::finish(EINSTEINRADIO_EOPT);
     }
   }

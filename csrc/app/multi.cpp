@@ -99,6 +99,11 @@ int MultiSession::open(const std::vector<std::string>& inputs, const SearchOptio
     else if (np > 1) dev = e;
     if ((rc = eng->init(dev, opt.batch > 0 ? opt.batch : 8))) return rc;
     if ((rc = eng->set_slots(static_cast<uint32_t>(inputs.size())))) return rc;
+    if (opt.ps_fp16 && !opt.white) {
+      log_message(LOG_ERROR, true, "The fp16 power spectrum needs whitening (-W).\n");
+      return RADPUL_EVAL;
+    }
+    eng->set_ps_fp16(opt.ps_fp16);
     d.engines.push_back(std::move(eng));
   }
   return 0;

@@ -107,6 +107,7 @@ SearchOptions dict_to_options(const py::dict& d) {
   if (d.contains("device")) o.device = d["device"].cast<int>();
   if (d.contains("batch")) o.batch = d["batch"].cast<int>();
   if (d.contains("use_cpu")) o.use_cpu = d["use_cpu"].cast<bool>();
+  if (d.contains("ps_fp16")) o.ps_fp16 = d["ps_fp16"].cast<bool>();
   if (d.contains("inputfile")) o.inputfile = d["inputfile"].cast<std::string>();
   if (d.contains("outputfile")) o.outputfile = d["outputfile"].cast<std::string>();
   if (d.contains("templatebank")) o.templatebank = d["templatebank"].cast<std::string>();

@@ -24,6 +24,7 @@ struct SearchOptions {
   int batch = 0;            // templates per device batch (0 = auto)
   bool use_cpu = false;     // CPU golden backend instead of HIP
   bool prewhitened = false; // series already whitened by another backend (DC removed)
+  bool ps_fp16 = false;     // store the power spectrum as fp16 (config 5; needs -W)
 };
 
 // Everything derived from the WU header + options (demod_binary.c:778-782,

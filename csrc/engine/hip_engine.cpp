@@ -156,6 +156,7 @@ struct HipEngine::Impl {
   bool ready = false;
   uint32_t p3_exp = 0;          // BRP_P3_EXP profiling switches (pass3_kernel)
   uint32_t num_cus = 256;
+  bool ps_fp16 = false;         // config 5: fp16 power spectrum between pass 3 and the harmonic sum
   uint32_t persist_per_cu = 4;  // persistent FFT passes: workgroups per CU (BRP_PERSIST, 0 = off)
   uint32_t ps_stride = 0;
   uint32_t i_start = 0;
@@ -302,6 +303,7 @@ struct HipEngine::Impl {
         a3.limit = std::min(g.harmonic_idx_hi, g.fft_size);
         a3.exp = p3_exp;
         a3.ps = ps.p;
+        a3.ps16 = ps_fp16 ? reinterpret_cast<_Float16*>(ps.p) : nullptr;
         a3.ps_stride = ps_stride;
         a3.norm = static_cast<float>(1.0 / g.nsamples);
         a3.tmpl = tmpl.p;
@@ -311,6 +313,7 @@ struct HipEngine::Impl {
       case kHarmonic: {
         hipk::HSArgs ah{};
         ah.ps = ps.p;
+        ah.ps16 = ps_fp16 ? reinterpret_cast<const _Float16*>(ps.p) : nullptr;
         ah.ps_stride = ps_stride;
         ah.w2 = g.window_2;
         ah.fhi = g.fundamental_idx_hi;
@@ -463,6 +466,14 @@ int HipEngine::set_slots(uint32_t k) {
 }
 
 uint32_t HipEngine::slots() const { return impl_->slots; }
+
+void HipEngine::set_ps_fp16(bool on) {
+  Impl& d = *impl_;
+  if (on == d.ps_fp16) return;
+  d.ps_fp16 = on;
+  for (auto& kv : d.graphs) (void)hipGraphExecDestroy(kv.second);  // captured arguments changed
+  d.graphs.clear();
+}
 
 int HipEngine::load_slot(uint32_t k, const std::vector<float>& series, float mu0) {
   Impl& d = *impl_;
@@ -830,6 +841,11 @@ class HipBackend final : public Backend {
       for (float v : series) mean += v;
       mean = series.empty() ? 0.0 : mean / series.size();
     }
+    if (opt.ps_fp16 && !(opt.white || opt.prewhitened)) {
+      log_message(LOG_ERROR, true, "The fp16 power spectrum needs whitening (-W): raw powers overflow fp16.\n");
+      return RADPUL_EVAL;
+    }
+    eng_.set_ps_fp16(opt.ps_fp16);
     int rc = eng_.setup(g, series, static_cast<float>(mean));
     if (rc) return rc;
     if (opt.white) return eng_.whiten(opt, zaps, series);

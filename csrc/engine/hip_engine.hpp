@@ -26,6 +26,9 @@ class HipEngine {
   // shape (set before setup(); setup() fills slot 0, load_slot() the others).
   // Templates pick their slot with TemplateInput::wu.
   int set_slots(uint32_t k);
+  // config 5: store the power spectrum as fp16 (halves the pass-3 write and the
+  // harmonic-sum reads; the sums stay fp32 in the reference order)
+  void set_ps_fp16(bool on);
   uint32_t slots() const;
   int load_slot(uint32_t k, const std::vector<float>& series, float mu0);
   // whitening + zapping of one slot on the device; `series` (that slot's raw

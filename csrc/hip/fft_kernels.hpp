@@ -89,6 +89,7 @@ struct Pass3Args {
   uint32_t limit;              // write bins k < limit only
   // P3_POWER
   float* ps;                   // [batch][ps_stride]
+  _Float16* ps16;              // fp16 spectrum instead of `ps` when non-null
   uint32_t ps_stride;
   float norm;                  // 1/N (float)
   const TemplateDev* tmpl;     // n_steps per template

@@ -339,6 +339,7 @@ __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Arg
   const bool correct = (MODE == P3_POWER) && n_s > 0 && !(a.exp & 2);
   float sink = 0.0f;
   float* ps = a.ps + static_cast<size_t>(b) * a.ps_stride;
+  _Float16* ps16 = a.ps16 ? a.ps16 + static_cast<size_t>(b) * a.ps_stride : nullptr;
   // X_k (+ delta * S_k) -> |X_k|^2 / N, or the complex bin
   // S_k = -(sin(pi n_s k/N) / sin(pi k/N)) e^{-i pi (n_s-1) k/N} from ta = W_2N^{n_s k}, tk = W_2N^k
   auto emit = [&](uint32_t k, float2 x, float2 tk, float2 ta) {
@@ -354,6 +355,7 @@ __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Arg
         p = (x.x * x.x + x.y * x.y) * a.norm;
       }
       if (a.exp & 1) sink += p;
+      else if (ps16) ps16[k] = static_cast<_Float16>(p);
       else ps[k] = p;
     } else {
       a.spec[k] = x;
@@ -389,7 +391,9 @@ __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Arg
             const float2 sp = padding_spectrum(a.tw, n_s, a.M);
             x = make_float2(x.x + dS * sp.x, x.y + dS * sp.y);
           }
-          ps[a.M] = (x.x * x.x + x.y * x.y) * a.norm;
+          const float pm = (x.x * x.x + x.y * x.y) * a.norm;
+          if (ps16) ps16[a.M] = static_cast<_Float16>(pm);
+          else ps[a.M] = pm;
         } else {
           a.spec[a.M] = x;
         }

@@ -44,11 +44,17 @@ __device__ __forceinline__ void emit(uint32_t* counter, uint2* list, uint32_t ca
   }
 }
 
+// T = float (exact path) or _Float16 (config 5 spectrum); every element is
+// widened to float before the reference-order float sums
+template <typename T>
 __global__ void __launch_bounds__(kThreads) harmonic_sum_kernel(HSArgs a) {
 #pragma clang fp contract(off)
   __shared__ __attribute__((aligned(16))) float sv[4][kSpanPad];  // S_1..S_4 over the tile + halo
   const int b = blockIdx.y;
-  const float* P = a.ps + static_cast<size_t>(b) * a.ps_stride;
+  const T* P = reinterpret_cast<const T*>(sizeof(T) == 4 ? static_cast<const void*>(a.ps)
+                                                        : static_cast<const void*>(a.ps16)) +
+               static_cast<size_t>(b) * a.ps_stride;
+  auto ld = [&](uint32_t idx) { return static_cast<float>(P[idx]); };
   const uint32_t i0 = a.i_start + blockIdx.x * kHsTile;
   const float ninf = -__builtin_inff();
 
@@ -56,15 +62,15 @@ __global__ void __launch_bounds__(kThreads) harmonic_sum_kernel(HSArgs a) {
     const uint32_t i = i0 + t;
     float s1 = ninf, s2 = ninf, s3 = ninf, s4 = ninf;
     if (i >= a.w2 && i < a.hhi) {
-      float sum = P[i];
-      sum += P[(8u * i + 8u) >> 4];
+      float sum = ld(i);
+      sum += ld((8u * i + 8u) >> 4);
       s1 = sum;
-      sum += P[(12u * i + 8u) >> 4] + P[(4u * i + 8u) >> 4];
+      sum += ld((12u * i + 8u) >> 4) + ld((4u * i + 8u) >> 4);
       s2 = sum;
-      sum += P[(14u * i + 8u) >> 4] + P[(10u * i + 8u) >> 4] + P[(6u * i + 8u) >> 4] + P[(2u * i + 8u) >> 4];
+      sum += ld((14u * i + 8u) >> 4) + ld((10u * i + 8u) >> 4) + ld((6u * i + 8u) >> 4) + ld((2u * i + 8u) >> 4);
       s3 = sum;
-      sum += P[(15u * i + 8u) >> 4] + P[(13u * i + 8u) >> 4] + P[(11u * i + 8u) >> 4] + P[(9u * i + 8u) >> 4] +
-             P[(7u * i + 8u) >> 4] + P[(5u * i + 8u) >> 4] + P[(3u * i + 8u) >> 4] + P[(i + 8u) >> 4];
+      sum += ld((15u * i + 8u) >> 4) + ld((13u * i + 8u) >> 4) + ld((11u * i + 8u) >> 4) + ld((9u * i + 8u) >> 4) +
+             ld((7u * i + 8u) >> 4) + ld((5u * i + 8u) >> 4) + ld((3u * i + 8u) >> 4) + ld((i + 8u) >> 4);
       s4 = sum;
     }
     sv[0][sidx(t)] = s1;
@@ -81,7 +87,7 @@ __global__ void __launch_bounds__(kThreads) harmonic_sum_kernel(HSArgs a) {
   for (int t = threadIdx.x; t < kHsTile; t += kThreads) {
     const uint32_t i = i0 + t;
     const bool in = (i >= a.w2 && i < a.fhi);
-    const float p = in ? P[i] : 0.0f;
+    const float p = in ? ld(i) : 0.0f;
     emit(count, list, a.cap, in && p > thr0, hs_pack(b, 0, i), p);
   }
   // levels 1..4: group of 2^h consecutive i starting at s == 2^(h-1) mod 2^h;
@@ -123,7 +129,10 @@ uint32_t hs_num_tiles(uint32_t i_start, uint32_t hhi) {
 hipError_t launch_harmonic_sum(const HSArgs& a, int batch, hipStream_t s) {
   const uint32_t tiles = hs_num_tiles(a.i_start, a.hhi);
   if (tiles == 0) return hipSuccess;
-  hipLaunchKernelGGL(harmonic_sum_kernel, dim3(tiles, batch), dim3(kThreads), 0, s, a);
+  if (a.ps16 != nullptr)
+    hipLaunchKernelGGL(harmonic_sum_kernel<_Float16>, dim3(tiles, batch), dim3(kThreads), 0, s, a);
+  else
+    hipLaunchKernelGGL(harmonic_sum_kernel<float>, dim3(tiles, batch), dim3(kThreads), 0, s, a);
   return hipGetLastError();
 }
 

@@ -12,6 +12,7 @@ constexpr int kHsTile = 1024;  // fundamental-level bins i per workgroup
 
 struct HSArgs {
   const float* ps;        // [batch][ps_stride]
+  const _Float16* ps16;   // fp16 spectrum (config 5) instead of `ps` when non-null
   uint32_t ps_stride;
   uint32_t w2, fhi, hhi;  // window_2, fundamental_idx_hi, harmonic_idx_hi
   uint32_t i_start;       // first i of tile 0 (== 8 mod 16, <= w2)

@@ -162,3 +162,14 @@ def test_multi_wu_batching_matches_single_runs(brp, gpu, tmp_path):
     for o in outs:
         lines, done = brp.read_results(o)
         assert done and lines
+
+
+def test_fp16_power_spectrum_config(brp, gpu, case, tmp_path):
+    """Config 5: fp16 spectrum between pass 3 and the harmonic sum. The strong
+    candidates are the fp32 ones (same bins), powers within fp16 rounding."""
+    f32 = BRPSearch(_cfg(case, tmp_path / "a")).run(write_output=False, use_checkpoint=False)
+    f16 = BRPSearch(_cfg(case, tmp_path / "b", ps_fp16=True)).run(write_output=False, use_checkpoint=False)
+    _compare_tables(f16.table, f32.table, rtol=3e-3)
+    with pytest.raises(RuntimeError):
+        BRPSearch(_cfg(case, tmp_path / "c", ps_fp16=True, white=False)).run(write_output=False,
+                                                                           use_checkpoint=False)
