@@ -230,8 +230,10 @@ struct HipEngine::Impl {
     v.assign(512, make_float2(0, 0));
     for (uint32_t i = 0; i < 512 && 256ull * i < L2L3; ++i) v[i] = root(256ull * i, L2L3);
     if ((rc = upload(t_p2hi, v))) return rc;
-    v.assign(4ull * L3, make_float2(0, 0));
-    for (uint32_t i = 0; i < 4 * L3; ++i) v[i] = root(i, 4ull * L3);
+    // pass 3: W_{4 L3}^j = hi[j >> 5] * lo[j & 31], stored as [lo 32 | hi 4 L3 / 32]
+    v.assign(32 + 4ull * L3 / 32, make_float2(0, 0));
+    for (uint32_t i = 0; i < 32; ++i) v[i] = root(i, 4ull * L3);
+    for (uint32_t m = 0; m < 4 * L3 / 32; ++m) v[32 + m] = root(32ull * m, 4ull * L3);
     return upload(t_p3, v);
   }
 

@@ -283,11 +283,15 @@ __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Arg
   constexpr int NT = NSLOT * TPC;
   constexpr int L4 = 4 * L;
   using Lay = BlockLayout<L, NSLOT, TPC, true>;
-  // data | stage twiddles W_L | W_{4L} (= W_2N^{C i})
-  __shared__ __attribute__((aligned(16))) float2 smem[Lay::kLds + kTwPad<L> + L4];
+  // data | stage twiddles W_L | W_{4L} (= W_2N^{C i}) as lo[32] | hi[4L/32]
+  constexpr int kT4 = 32 + L4 / 32;
+  static_assert(L4 % 32 == 0, "two-level W_{4L} table");
+  __shared__ __attribute__((aligned(16))) float2 smem[Lay::kLds + kTwPad<L> + kT4];
   float2* data = smem;
   float2* twl = smem + Lay::kLds;
   float2* t4 = twl + kTwPad<L>;
+  // W_{4L}^j, j < 4L
+  auto w4 = [&](uint32_t j) { return cmul(t4[32 + (j >> 5)], t4[j & 31u]); };
 
   const int b = blockIdx.y;
   const float2* buf = a.buf + static_cast<size_t>(b) * a.M;
@@ -309,9 +313,7 @@ __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Arg
   }
   copy_stage_twiddles<L>(twl, a.tb.st3);
   {
-    const float4* t4s = reinterpret_cast<const float4*>(a.tb.p3);
-    float4* t4d = reinterpret_cast<float4*>(t4);
-    for (int i = threadIdx.x; i < L4 / 2; i += NT) t4d[i] = t4s[i];
+    for (int i = threadIdx.x; i < kT4; i += NT) t4[i] = a.tb.p3[i];
   }
   // mean-padding correction delta = (sum of (sample - mu0)) / n_steps (pass 2)
   double delta = 0.0;
@@ -371,10 +373,10 @@ __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Arg
       const int k3m = (c == 0) ? (L - k3) % L : L - 1 - k3;
       const float2 zm = data[Lay::idx(k3m, c == 0 ? s : ROWS + s)];
       const uint32_t k = c + a.C * static_cast<uint32_t>(k3);
-      const float2 tk = cmul(rt.t1, t4[k3]);  // W_2N^k
+      const float2 tk = cmul(rt.t1, w4(static_cast<uint32_t>(k3)));  // W_2N^k
       const float2 w = cmul(tk, tk);          // W_N^k
       float2 ta = make_float2(0.f, 0.f);
-      if (correct) ta = cmul(rt.ta, t4[(n_s * static_cast<uint32_t>(k3)) % L4]);
+      if (correct) ta = cmul(rt.ta, w4((n_s * static_cast<uint32_t>(k3)) % L4));
       emit(k, untangle_w(zk, zm, w), tk, ta);
       if (c != 0 && c != half) {
         const uint32_t kk = a.M - k;                 // = cm + C*(L-1-k3)
