@@ -99,13 +99,17 @@ __global__ void __launch_bounds__(kNcol * tpc_for<L>()) pass1_kernel(Pass1Args a
     float raw[2 * kPer];
 #pragma unroll
     for (int e = 0; e < 2 * kPer; ++e) raw[e] = series[idx[e] < 0 ? 0 : idx[e]];
+    // per-thread partial sum in float (<= 2 kPer samples of the centred
+    // series), widened once for the deterministic block reduction
+    float fsum = 0.0f;
 #pragma unroll
     for (int u = 0; u < kPer; ++u) {
       const float x0 = idx[2 * u] < 0 ? 0.0f : raw[2 * u] - td.mu0;
       const float x1 = idx[2 * u + 1] < 0 ? 0.0f : raw[2 * u + 1] - td.mu0;
-      sum += static_cast<double>(x0) + static_cast<double>(x1);
+      fsum += x0 + x1;
       data[Lay::idx(tj + u * TPC, c)] = make_float2(x0, x1);
     }
+    sum = static_cast<double>(fsum);
   } else if (MODE == P1_REAL) {
     for (int r = tj; r < L; r += TPC) {
       const uint32_t n = r * a.L2L3 + col_base + c;
