@@ -203,6 +203,34 @@ __device__ __forceinline__ void block_stage(float2* lds, const float2* tw_lds) {
   __syncthreads();
 }
 
+// First stage (Ns = 1, no twiddles) of radix R on data whose rows >= L/R are
+// zero: the DFT of (x, 0, ..., 0) is (x, ..., x), so the stage copies row j to
+// rows R j .. R j + R - 1 (the zero rows are never read).
+template <int L, int NCOL, int TPC, bool ROWMAJOR, int R>
+__device__ __forceinline__ void block_stage_replicate(float2* lds) {
+  using Lay = BlockLayout<L, NCOL, TPC, ROWMAJOR>;
+  constexpr int kBf = L / R;
+  constexpr int kNb = (kBf + TPC - 1) / TPC;
+  int c, tj;
+  Lay::coords(threadIdx.x, c, tj);
+  float2 v[kNb];
+#pragma unroll
+  for (int u = 0; u < kNb; ++u) {
+    const int j = tj + u * TPC;
+    if (kBf % TPC == 0 || j < kBf) v[u] = lds[Lay::idx(j, c)];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < kNb; ++u) {
+    const int j = tj + u * TPC;
+    if (kBf % TPC == 0 || j < kBf) {
+#pragma unroll
+      for (int q = 0; q < R; ++q) lds[Lay::idx(R * j + q, c)] = v[u];
+    }
+  }
+  __syncthreads();
+}
+
 template <int L, int NCOL, int TPC, bool ROWMAJOR, int Ns, int... Rs>
 struct BlockStages;
 
@@ -261,6 +289,19 @@ struct BlockFFT {
   };
   static __device__ __forceinline__ void run(float2* lds, const float2* tw) {
     Radices<L>::template apply<Impl>::run(lds, tw);
+  }
+  // rows >= L / R0 are zero (R0 = first radix): replicate instead of stage 1
+  template <int R0, int... Rs>
+  struct ImplPruned {
+    static constexpr int kFirst = R0;
+    static __device__ __forceinline__ void run(float2* lds, const float2* tw) {
+      block_stage_replicate<L, NCOL, TPC, ROWMAJOR, R0>(lds);
+      BlockStages<L, NCOL, TPC, ROWMAJOR, R0, Rs...>::run(lds, tw);
+    }
+  };
+  static constexpr int kFirstRadix = Radices<L>::template apply<ImplPruned>::kFirst;
+  static __device__ __forceinline__ void run_pruned(float2* lds, const float2* tw) {
+    Radices<L>::template apply<ImplPruned>::run(lds, tw);
   }
 };
 

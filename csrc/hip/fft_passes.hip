@@ -66,6 +66,7 @@ __global__ void __launch_bounds__(kNcol * tpc_for<L>()) pass1_kernel(Pass1Args a
   Lay::coords(threadIdx.x, c, tj);
 
   double sum = 0.0;
+  bool pruned = false;
   if (MODE == P1_RESAMPLE) {
     __shared__ float lut_s[kLutSize], lut_c[kLutSize];
     for (int i = threadIdx.x; i < kLutSize; i += NT) {
@@ -76,12 +77,18 @@ __global__ void __launch_bounds__(kNcol * tpc_for<L>()) pass1_kernel(Pass1Args a
     const bool fast = a.n_unpadded <= (1u << 23);
     const TemplateDev td = a.tmpl[b];
     const float* series = a.series + static_cast<size_t>(td.wu) * a.n_unpadded;
+    // With padding >= R0 (the first radix) every row n1 >= L/R0 of the
+    // tile lies in the zero padding: those rows are neither resampled nor
+    // stored, and the FFT's first stage replicates (BlockFFT::run_pruned).
+    constexpr int kR0 = BlockFFT<L, kNcol, TPC, false>::kFirstRadix;
+    pruned = 2ull * (L / kR0) * a.L2L3 >= td.n_steps;
     // three phases so that all gathers of the thread are in flight together:
     // nearest indices (LUT sine, VALU), unconditional clamped loads, then
     // select/centre/accumulate into LDS
     constexpr int kPer = L / TPC;
     const int last = static_cast<int>(a.n_unpadded) - 1;
     int idx[2 * kPer];
+    const int rows = pruned ? L / kR0 : L;
 #pragma unroll
     for (int u = 0; u < kPer; ++u) {
       const uint32_t m0 = 2 * ((tj + u * TPC) * a.L2L3 + col_base + c);
@@ -89,7 +96,7 @@ __global__ void __launch_bounds__(kNcol * tpc_for<L>()) pass1_kernel(Pass1Args a
       for (int q = 0; q < 2; ++q) {
         const uint32_t m = m0 + q;
         int i = -1;
-        if (m < td.n_steps) {
+        if (tj + u * TPC < rows && m < td.n_steps) {
           const float dt = resamp_del_t(m, td.p, lut_s, lut_c);
           i = min(max(fast ? resamp_nearest_f(m, dt) : resamp_nearest(m, dt), 0), last);
         }
@@ -107,7 +114,7 @@ __global__ void __launch_bounds__(kNcol * tpc_for<L>()) pass1_kernel(Pass1Args a
       const float x0 = idx[2 * u] < 0 ? 0.0f : raw[2 * u] - td.mu0;
       const float x1 = idx[2 * u + 1] < 0 ? 0.0f : raw[2 * u + 1] - td.mu0;
       fsum += x0 + x1;
-      data[Lay::idx(tj + u * TPC, c)] = make_float2(x0, x1);
+      if (tj + u * TPC < rows) data[Lay::idx(tj + u * TPC, c)] = make_float2(x0, x1);
     }
     sum = static_cast<double>(fsum);
   } else if (MODE == P1_REAL) {
@@ -126,7 +133,8 @@ __global__ void __launch_bounds__(kNcol * tpc_for<L>()) pass1_kernel(Pass1Args a
   copy_stage_twiddles<L>(twl, a.tb.st1);
   for (int k1 = threadIdx.x; k1 < L; k1 += NT) two[k1] = a.tb.p1[n2 * L + k1];  // W_{L1 L2}^{n2 k1}
   __syncthreads();
-  BlockFFT<L, kNcol, TPC, false>::run(data, twl);
+  if (pruned) BlockFFT<L, kNcol, TPC, false>::run_pruned(data, twl);
+  else BlockFFT<L, kNcol, TPC, false>::run(data, twl);
 
   float2* out = a.out + static_cast<size_t>(b) * M;
   for (int k1 = tj; k1 < L; k1 += TPC) {
