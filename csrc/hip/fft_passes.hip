@@ -9,6 +9,7 @@
 // opencl/app/demod_binary_ocl.cpp:972-1314, demod_binary_fft_fftw.c:46-113) and
 // its resampling kernels (cuda/app/demod_binary_cuda.cuh:69-184).
 #include <algorithm>
+#include <type_traits>
 
 #include "fft_block.hpp"
 #include "fft_kernels.hpp"
@@ -84,38 +85,48 @@ __global__ void __launch_bounds__(kNcol * tpc_for<L>()) pass1_kernel(Pass1Args a
     pruned = 2ull * (L / kR0) * a.L2L3 >= td.n_steps;
     // three phases so that all gathers of the thread are in flight together:
     // nearest indices (LUT sine, VALU), unconditional clamped loads, then
-    // select/centre/accumulate into LDS
-    constexpr int kPer = L / TPC;
+    // select/centre/accumulate into LDS. NU = row iterations of the thread
+    // (all L rows, or the L/R0 rows outside the padding).
     const int last = static_cast<int>(a.n_unpadded) - 1;
-    int idx[2 * kPer];
-    const int rows = pruned ? L / kR0 : L;
+    const int rows_valid = pruned ? L / kR0 : L;
+    auto gather = [&](auto nu_tag) {
+      constexpr int NU = decltype(nu_tag)::value;
+      constexpr int ROWS = NU * TPC;
+      int idx[2 * NU];
 #pragma unroll
-    for (int u = 0; u < kPer; ++u) {
-      const uint32_t m0 = 2 * ((tj + u * TPC) * a.L2L3 + col_base + c);
+      for (int u = 0; u < NU; ++u) {
+        const int r = tj + u * TPC;
+        const uint32_t m0 = 2 * (r * a.L2L3 + col_base + c);
 #pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const uint32_t m = m0 + q;
-        int i = -1;
-        if (tj + u * TPC < rows && m < td.n_steps) {
-          const float dt = resamp_del_t(m, td.p, lut_s, lut_c);
-          i = min(max(fast ? resamp_nearest_f(m, dt) : resamp_nearest(m, dt), 0), last);
+        for (int q = 0; q < 2; ++q) {
+          const uint32_t m = m0 + q;
+          int i = -1;
+          if ((ROWS == L || r < rows_valid) && m < td.n_steps) {
+            const float dt = resamp_del_t(m, td.p, lut_s, lut_c);
+            i = min(max(fast ? resamp_nearest_f(m, dt) : resamp_nearest(m, dt), 0), last);
+          }
+          idx[2 * u + q] = i;
         }
-        idx[2 * u + q] = i;
       }
-    }
-    float raw[2 * kPer];
+      float raw[2 * NU];
 #pragma unroll
-    for (int e = 0; e < 2 * kPer; ++e) raw[e] = series[idx[e] < 0 ? 0 : idx[e]];
-    // per-thread partial sum in float (<= 2 kPer samples of the centred
-    // series), widened once for the deterministic block reduction
-    float fsum = 0.0f;
+      for (int e = 0; e < 2 * NU; ++e) raw[e] = series[idx[e] < 0 ? 0 : idx[e]];
+      // per-thread partial sum in float, widened once for the block reduction
+      float fsum = 0.0f;
 #pragma unroll
-    for (int u = 0; u < kPer; ++u) {
-      const float x0 = idx[2 * u] < 0 ? 0.0f : raw[2 * u] - td.mu0;
-      const float x1 = idx[2 * u + 1] < 0 ? 0.0f : raw[2 * u + 1] - td.mu0;
-      fsum += x0 + x1;
-      if (tj + u * TPC < rows) data[Lay::idx(tj + u * TPC, c)] = make_float2(x0, x1);
-    }
+      for (int u = 0; u < NU; ++u) {
+        const int r = tj + u * TPC;
+        const float x0 = idx[2 * u] < 0 ? 0.0f : raw[2 * u] - td.mu0;
+        const float x1 = idx[2 * u + 1] < 0 ? 0.0f : raw[2 * u + 1] - td.mu0;
+        fsum += x0 + x1;
+        if (ROWS == L || r < rows_valid) data[Lay::idx(r, c)] = make_float2(x0, x1);
+      }
+      return fsum;
+    };
+    constexpr int kPer = L / TPC;
+    constexpr int kPerPruned = (L / kR0 + TPC - 1) / TPC;
+    const float fsum = pruned ? gather(std::integral_constant<int, kPerPruned>{})
+                              : gather(std::integral_constant<int, kPer>{});
     sum = static_cast<double>(fsum);
   } else if (MODE == P1_REAL) {
     for (int r = tj; r < L; r += TPC) {
