@@ -390,16 +390,30 @@ __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Arg
   // untangle: thread -> (slot s, k3 stream), rows c <= C/2 own their bins;
   // bin M-k of the mirror row reuses the twiddles of bin k:
   //   W_2N^{M-k} = -i conj(W_2N^k),  W_2N^{n_s (M-k)} = (-i)^{n_s} conj(W_2N^{n_s k})
+  // The thread's bins k3 = t + kStreams * it advance the twiddles by fixed
+  // rotations: W_2N^k and W_2N^{n_s k} are stepped by one complex multiply per
+  // bin (a few ulp over L / kStreams steps) instead of two table products.
+  static_assert(L % kStreams == 0, "whole untangle iterations");
   if (c <= half) {
-    for (int k3 = t; k3 < L; k3 += kStreams) {
+    float2 tk = cmul(rt.t1, w4(static_cast<uint32_t>(t)));  // W_2N^k for k3 = t
+    const float2 tk_step = w4(static_cast<uint32_t>(kStreams));
+    float2 ta = make_float2(0.f, 0.f), ta_step = make_float2(1.f, 0.f);
+    if (correct) {
+      ta = cmul(rt.ta, w4((n_s * static_cast<uint32_t>(t)) % L4));
+      ta_step = w4((n_s * static_cast<uint32_t>(kStreams)) % L4);
+    }
+#pragma unroll
+    for (int it = 0; it < L / kStreams; ++it) {
+      const int k3 = t + it * kStreams;
+      if (it > 0) {
+        tk = cmul(tk, tk_step);
+        if (correct) ta = cmul(ta, ta_step);
+      }
       const float2 zk = data[Lay::idx(k3, s)];
       const int k3m = (c == 0) ? (L - k3) % L : L - 1 - k3;
       const float2 zm = data[Lay::idx(k3m, c == 0 ? s : ROWS + s)];
       const uint32_t k = c + a.C * static_cast<uint32_t>(k3);
-      const float2 tk = cmul(rt.t1, w4(static_cast<uint32_t>(k3)));  // W_2N^k
       const float2 w = cmul(tk, tk);          // W_N^k
-      float2 ta = make_float2(0.f, 0.f);
-      if (correct) ta = cmul(rt.ta, w4((n_s * static_cast<uint32_t>(k3)) % L4));
       emit(k, untangle_w(zk, zm, w), tk, ta);
       if (c != 0 && c != half) {
         const uint32_t kk = a.M - k;                 // = cm + C*(L-1-k3)
