@@ -154,7 +154,6 @@ struct HipEngine::Impl {
   SearchGeometry g;
   FFTPlan3 plan;
   bool ready = false;
-  uint32_t p3_exp = 0;          // BRP_P3_EXP profiling switches (pass3_kernel)
   uint32_t num_cus = 256;
   bool ps_fp16 = false;         // config 5: fp16 power spectrum between pass 3 and the harmonic sum
   uint32_t persist_per_cu = 4;  // persistent FFT passes: workgroups per CU (BRP_PERSIST, 0 = off)
@@ -274,7 +273,6 @@ struct HipEngine::Impl {
         a1.n_unpadded = g.n_unpadded;
         a1.tmpl = tmpl.p;
         a1.partials = partials.p;
-        a1.exp = p3_exp;
         return hipk::launch_pass1(plan, hipk::P1_RESAMPLE, a1, nb, stream);
       }
       case kPass2: {
@@ -289,7 +287,6 @@ struct HipEngine::Impl {
         a2.n_partials = plan.wg1();
         a2.tmpl = tmpl.p;
         a2.delta = delta.p;
-        a2.exp = p3_exp;
         return hipk::launch_pass2(plan, a2, nb, stream);
       }
       case kPass3: {
@@ -303,7 +300,6 @@ struct HipEngine::Impl {
         a3.tw = tw;
         a3.tb = tables();
         a3.limit = std::min(g.harmonic_idx_hi, g.fft_size);
-        a3.exp = p3_exp;
         a3.ps = ps.p;
         a3.ps16 = ps_fp16 ? reinterpret_cast<_Float16*>(ps.p) : nullptr;
         a3.ps_stride = ps_stride;
@@ -354,7 +350,6 @@ int HipEngine::init(int device, int batch) {
     log_message(LOG_ERROR, true, "No HIP device available.\n");
     return RADPUL_HIP_DEVICE_FIND;
   }
-  if (const char* e = std::getenv("BRP_P3_EXP")) impl_->p3_exp = static_cast<uint32_t>(std::atoi(e));
   if (device < 0) {
     const char* env = std::getenv("BRP_DEVICE");
     device = env ? std::atoi(env) : 0;

@@ -57,7 +57,6 @@ struct Pass1Args {
   uint32_t n_real;
   // P1_COMPLEX_CONJ
   const float2* cplx_in;
-  uint32_t exp;                // profiling experiments (BRP_P3_EXP), 0 in production
 };
 
 struct Pass2Args {
@@ -72,12 +71,12 @@ struct Pass2Args {
   uint32_t n_partials;
   const TemplateDev* tmpl;
   double* delta;               // [batch]
-  uint32_t exp;                // profiling experiments (BRP_P3_EXP), 0 in production
 };
 
 enum Pass3Mode : int {
   P3_POWER = 0,     // untangle + power spectrum (+ mean-padding correction)
   P3_COMPLEX = 1,   // untangle, complex half spectrum out (whitening)
+  P3_POWER16 = 2,   // as P3_POWER, fp16 spectrum (Pass3Args::ps16; selected by launch_pass3)
 };
 
 struct Pass3Args {
@@ -96,7 +95,6 @@ struct Pass3Args {
   const double* delta;         // [batch] mean-padding correction (pass 2)
   // P3_COMPLEX
   float2* spec;                // fft_size complex bins
-  uint32_t exp;                // profiling experiments (BRP_P3_EXP), 0 in production
 };
 
 // plain row pass of the inverse transform: conj, scale, write the first

@@ -202,7 +202,7 @@ __global__ void __launch_bounds__(kNcol * tpc_for<L>(), kMinWaves) pass2_kernel(
 #pragma unroll
     for (int u = 0; u < kPer; ++u) pre[u] = src[static_cast<size_t>(tj + u * TPC) * a.L3 + c];
   }
-  if (!(a.exp & 64)) {
+  {
     copy_stage_twiddles<L>(twl, a.tb.st2);
     const uint32_t nhi = (a.L2L3 + kLo - 1) / kLo;
     for (int i = threadIdx.x; i < kLo; i += NT) lo[i] = a.tb.p2lo[i];
@@ -224,13 +224,13 @@ __global__ void __launch_bounds__(kNcol * tpc_for<L>(), kMinWaves) pass2_kernel(
       for (int u = 0; u < kPer; ++u) pre[u] = src[static_cast<size_t>(tj + u * TPC) * a.L3 + c];
     }
     __syncthreads();
-    if (!(a.exp & 16)) BlockFFT<L, kNcol, TPC, false>::run(data, twl);
+    BlockFFT<L, kNcol, TPC, false>::run(data, twl);
 #pragma unroll
     for (int u = 0; u < kPer; ++u) {
       const int k2 = tj + u * TPC;
       const uint32_t e = n3 * static_cast<uint32_t>(k2);  // < L2*L3
       float2 v = data[Lay::idx(k2, c)];
-      if (!(a.exp & 32)) v = cmul(v, cmul(wc, cmul(hi[e >> kP2LoBits], lo[e & (kLo - 1)])));
+      v = cmul(v, cmul(wc, cmul(hi[e >> kP2LoBits], lo[e & (kLo - 1)])));
       base[static_cast<size_t>(k2) * a.L3 + c] = v;
     }
     if (a.partials != nullptr && rem == 0) {
@@ -341,7 +341,7 @@ __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Arg
   // mean-padding correction delta = (sum of (sample - mu0)) / n_steps (pass 2)
   double delta = 0.0;
   uint32_t n_s = 0;
-  if (MODE == P3_POWER) {
+  if (MODE == P3_POWER || MODE == P3_POWER16) {
     n_s = a.tmpl[b].n_steps;
     delta = a.delta[b];
   }
@@ -354,33 +354,28 @@ __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Arg
   const uint32_t half = a.C / 2;
   const RowTw rt = row_twiddles(a.tw, c, n_s);
   __syncthreads();
-  if (!(a.exp & 4)) BlockFFT<L, NSLOT, TPC, true>::run(data, twl);
-  if (a.exp & 8) {
-    if (data[Lay::idx(t, s)].x == 12345.0f) a.ps[threadIdx.x] = 1.0f;
-    return;
-  }
+  BlockFFT<L, NSLOT, TPC, true>::run(data, twl);
 
   const float dS = static_cast<float>(delta);
-  const bool correct = (MODE == P3_POWER) && n_s > 0 && !(a.exp & 2);
-  float sink = 0.0f;
+  constexpr bool kPower = (MODE == P3_POWER || MODE == P3_POWER16);
+  const bool correct = kPower && n_s > 0;
   float* ps = a.ps + static_cast<size_t>(b) * a.ps_stride;
   _Float16* ps16 = a.ps16 ? a.ps16 + static_cast<size_t>(b) * a.ps_stride : nullptr;
   // X_k (+ delta * S_k) -> |X_k|^2 / N, or the complex bin
   // S_k = -(sin(pi n_s k/N) / sin(pi k/N)) e^{-i pi (n_s-1) k/N} from ta = W_2N^{n_s k}, tk = W_2N^k
   auto emit = [&](uint32_t k, float2 x, float2 tk, float2 ta) {
     if (k >= a.limit) return;
-    if (MODE == P3_POWER) {
+    if (kPower) {
       float p = 0.0f;
       if (k != 0) {
         if (correct) {
-          const float ratio = __fdividef(ta.y, tk.y);
+          const float ratio = ta.y * __builtin_amdgcn_rcpf(tk.y);  // v_rcp_f32 (1 ulp)
           const float2 tc = cmul(ta, conjf2(tk));  // W_2N^{(n_s-1) k}
           x = make_float2(x.x - dS * ratio * tc.x, x.y - dS * ratio * tc.y);
         }
         p = (x.x * x.x + x.y * x.y) * a.norm;
       }
-      if (a.exp & 1) sink += p;
-      else if (ps16) ps16[k] = static_cast<_Float16>(p);
+      if (MODE == P3_POWER16) ps16[k] = static_cast<_Float16>(p);
       else ps[k] = p;
     } else {
       a.spec[k] = x;
@@ -425,13 +420,13 @@ __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Arg
       if (c == 0 && k3 == 0 && a.M < a.limit) {
         // Nyquist bin M: X_M = Re Z_0 - Im Z_0
         float2 x = make_float2(zk.x - zk.y, 0.0f);
-        if (MODE == P3_POWER) {
+        if (kPower) {
           if (correct) {
             const float2 sp = padding_spectrum(a.tw, n_s, a.M);
             x = make_float2(x.x + dS * sp.x, x.y + dS * sp.y);
           }
           const float pm = (x.x * x.x + x.y * x.y) * a.norm;
-          if (ps16) ps16[a.M] = static_cast<_Float16>(pm);
+          if (MODE == P3_POWER16) ps16[a.M] = static_cast<_Float16>(pm);
           else ps[a.M] = pm;
         } else {
           a.spec[a.M] = x;
@@ -439,7 +434,6 @@ __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Arg
       }
     }
   }
-  if ((a.exp & 1) && sink == 12345.0f) a.ps[threadIdx.x] = sink;
 }
 
 template <int L, int ROWS>
@@ -544,7 +538,9 @@ hipError_t launch_pass3(const FFTPlan3& plan, Pass3Mode mode, const Pass3Args& a
 #define X(n)                                                                                              \
   case n: {                                                                                               \
     const dim3 block(2 * kRows3 * tpc_for<n>());                                                          \
-    if (mode == P3_POWER) hipLaunchKernelGGL((pass3_kernel<n, kRows3, P3_POWER>), grid, block, 0, s, a);  \
+    if (mode == P3_POWER && a.ps16)                                                                       \
+      hipLaunchKernelGGL((pass3_kernel<n, kRows3, P3_POWER16>), grid, block, 0, s, a);                    \
+    else if (mode == P3_POWER) hipLaunchKernelGGL((pass3_kernel<n, kRows3, P3_POWER>), grid, block, 0, s, a); \
     else hipLaunchKernelGGL((pass3_kernel<n, kRows3, P3_COMPLEX>), grid, block, 0, s, a);                 \
     break;                                                                                                \
   }
