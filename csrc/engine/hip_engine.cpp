@@ -406,6 +406,8 @@ int HipEngine::setup(const SearchGeometry& g, const std::vector<float>& series, 
   }
   if (const char* e = std::getenv("BRP_PERSIST")) d.persist_per_cu = static_cast<uint32_t>(std::atoi(e));
   d.plan.persist_wgs = d.persist_per_cu * d.num_cus;
+  d.plan.legacy_pass1 = std::getenv("BRP_P1_LEGACY") != nullptr;
+  d.plan.legacy_pass2 = std::getenv("BRP_P2_LEGACY") != nullptr;
   log_message(LOG_DEBUG, true, "FFT plan: N=%u M=%u = %u x %u x %u\n", g.nsamples, d.plan.M, d.plan.L1, d.plan.L2,
               d.plan.L3);
   const uint32_t limit = std::min(g.harmonic_idx_hi, g.fft_size);

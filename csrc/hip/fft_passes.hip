@@ -158,6 +158,111 @@ __global__ void __launch_bounds__(kNcol * tpc_for<L>()) pass1_kernel(Pass1Args a
   }
 }
 
+// Resampling pass 1 for L = 3 * R2 * 16 when the padding is at least 3x
+// (every row n1 >= L/3 of a column lies in the zero padding). Stage 1 (radix
+// 3 on rows that are zero beyond L/3) replicates, so stage 1 + stage 2 (radix
+// R2, Ns = 3) of butterfly group g = j/3 read only the gathered rows
+// g + 16 q (q < R2) and produce rows 12 g .. 12 g + 3 R2 - 1: one thread per
+// group gathers exactly its inputs and computes the three radix-R2
+// butterflies in registers. The tile crosses LDS once; the last stage (radix
+// 16, Ns = 3 R2) stores its natural-order rows k1 = j + 3 R2 q straight to
+// global memory with the output twiddle W_{L1 L2}^{n2 k1}.
+template <int R2>
+__global__ void __launch_bounds__(kNcol * 16) pass1_pruned3_kernel(Pass1Args a) {
+  constexpr int L = 3 * R2 * 16;
+  constexpr int TPC = 16;               // threads per column = butterfly groups of stages 1+2
+  constexpr int NT = kNcol * TPC;
+  constexpr int NB3 = 3 * R2;           // last-stage butterflies per column (threads tj < NB3)
+  static_assert(NB3 <= TPC, "one last-stage butterfly per thread");
+  __shared__ __attribute__((aligned(16))) float2 data[L * kNcol];
+  __shared__ float2 wl[L];              // W_L^e
+  __shared__ float2 two[L];             // W_{L1 L2}^{n2 k1}
+  __shared__ float lut_s[kLutSize], lut_c[kLutSize];
+  __shared__ double red[NT / kWave + 1];
+
+  const int b = blockIdx.y;
+  const uint32_t nblk3 = a.L3 / kNcol;
+  const uint32_t n2 = blockIdx.x / nblk3;
+  const uint32_t col_base = n2 * a.L3 + (blockIdx.x % nblk3) * kNcol;
+  const size_t M = static_cast<size_t>(L) * a.L2L3;
+  const int c = threadIdx.x % kNcol;
+  const int tj = threadIdx.x / kNcol;
+
+  for (int i = threadIdx.x; i < kLutSize; i += NT) {
+    lut_s[i] = kSinLut[i];
+    lut_c[i] = kCosLut[i];
+  }
+  for (int e = threadIdx.x; e < L; e += NT) {
+    wl[e] = a.tb.st1[e + (e >> 4)];
+    two[e] = a.tb.p1[n2 * L + e];
+  }
+  __syncthreads();
+
+  // gather rows g + 16 q (q < R2) of column c: nearest-neighbour resampling
+  // with the reference's float arithmetic (three phases keep all loads in flight)
+  const bool fast = a.n_unpadded <= (1u << 23);
+  const TemplateDev td = a.tmpl[b];
+  const float* series = a.series + static_cast<size_t>(td.wu) * a.n_unpadded;
+  const int last = static_cast<int>(a.n_unpadded) - 1;
+  int idx[2 * R2];
+#pragma unroll
+  for (int q = 0; q < R2; ++q) {
+    const uint32_t m0 = 2 * ((tj + 16 * q) * a.L2L3 + col_base + c);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const uint32_t m = m0 + h;
+      int i = -1;
+      if (m < td.n_steps) {
+        const float dt = resamp_del_t(m, td.p, lut_s, lut_c);
+        i = min(max(fast ? resamp_nearest_f(m, dt) : resamp_nearest(m, dt), 0), last);
+      }
+      idx[2 * q + h] = i;
+    }
+  }
+  float raw[2 * R2];
+#pragma unroll
+  for (int e = 0; e < 2 * R2; ++e) raw[e] = series[idx[e] < 0 ? 0 : idx[e]];
+  float fsum = 0.0f;
+  float2 x[R2];
+#pragma unroll
+  for (int q = 0; q < R2; ++q) {
+    const float x0 = idx[2 * q] < 0 ? 0.0f : raw[2 * q] - td.mu0;
+    const float x1 = idx[2 * q + 1] < 0 ? 0.0f : raw[2 * q + 1] - td.mu0;
+    fsum += x0 + x1;
+    x[q] = make_float2(x0, x1);
+  }
+  // stages 1+2: butterfly j = 3 tj + s (s < 3) is a radix-R2 DFT of the
+  // group's rows with twiddle W_{3 R2}^{s q} = W_L^{16 s q}; its outputs
+  // are rows 12 tj + s + 3 q
+#pragma unroll
+  for (int s = 0; s < 3; ++s) {
+    float2 y[R2];
+#pragma unroll
+    for (int q = 0; q < R2; ++q) y[q] = (s == 0 || q == 0) ? x[q] : cmul(x[q], wl[(16 * s * q) % L]);
+    Dft<R2>::run(y);
+#pragma unroll
+    for (int q = 0; q < R2; ++q) data[(NB3 * tj + s + 3 * q) * kNcol + c] = y[q];
+  }
+  __syncthreads();
+  // stage 3 (radix 16, Ns = 3 R2): butterfly j = tj reads rows j + NB3 q
+  if (tj < NB3) {
+    float2 z[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) z[q] = data[(tj + NB3 * q) * kNcol + c];
+#pragma unroll
+    for (int q = 1; q < 16; ++q) z[q] = cmul(z[q], wl[tj * q]);
+    Dft<16>::run(z);
+    float2* out = a.out + static_cast<size_t>(b) * M + col_base + c;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int k1 = tj + NB3 * q;
+      out[static_cast<size_t>(k1) * a.L2L3] = cmul(z[q], two[k1]);
+    }
+  }
+  const double tot = block_sum<NT>(static_cast<double>(fsum), red);
+  if (threadIdx.x == 0) a.partials[static_cast<size_t>(b) * gridDim.x + blockIdx.x] = tot;
+}
+
 // ------------------------------------------------------------------ pass 2
 // at least kMinWaves waves per SIMD: keeps the unrolled prefetch + FFT code
 // within 256 VGPRs (no spills) at 2 waves/SIMD
@@ -245,6 +350,123 @@ __global__ void __launch_bounds__(kNcol * tpc_for<L>(), kMinWaves) pass2_kernel(
       }
     }
     __syncthreads();  // LDS tile free for the next iteration
+    tile = next;
+  }
+}
+
+// Register-staged pass 2 for L = R1 * 16 with R1 | 16 (L in 32..256), the
+// two-stage radix (R1, 16) transform of 16 columns. The columns a thread loads
+// (rows tj + TPC u) are exactly the inputs of its stage-1 butterflies, and the
+// rows its stage-2 butterfly produces (k2 = tj + TPC q) are exactly the rows it
+// stores, so the tile crosses LDS once (stage 1 -> stage 2) instead of four
+// times, with two barriers per tile. The output twiddle
+// W_M^{n3 (k1 + L1 k2)} = wc * W_{L2L3}^{n3 tj} * (W_{L2L3}^{n3 TPC})^q is
+// evaluated exactly at q = 0 and q = 8 and stepped by one rotation in between.
+template <int L>
+__global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_per_eu(3, 8))) pass2r_kernel(Pass2Args a, uint32_t ntiles) {
+  constexpr int R1 = L / 16;
+  constexpr int TPC = R1;
+  constexpr int NT = kNcol * TPC;
+  constexpr int NB1 = 16 / R1;  // stage-1 butterflies per thread
+  static_assert(R1 >= 2 && 16 % R1 == 0, "L = R1 * 16 with R1 | 16");
+  constexpr int kLo = 1 << kP2LoBits;
+  __shared__ __attribute__((aligned(16))) float2 data[L * kNcol];
+  __shared__ float2 wl[L];  // W_L^e
+  __shared__ double red[NT / kWave + 1];
+  const float2* lo = a.tb.p2lo;  // three exact lookups per tile: served by L1/L2
+  const float2* hi = a.tb.p2hi;
+
+  const uint32_t nblk3 = a.L3 / kNcol;
+  const uint32_t per_b = a.L1 * nblk3;
+  const size_t M = static_cast<size_t>(a.L1) * a.L2L3;
+  const int c = threadIdx.x % kNcol;
+  const int tj = threadIdx.x / kNcol;
+  // wave-uniform tile origin, kept in SGPRs (the runtime divisions are VALU
+  // sequences; readfirstlane lets every load/store use an SGPR base + 32-bit offset)
+  auto tile_base = [&](uint32_t tl) -> const float2* {
+    const uint32_t b = tl / per_b, rem = tl % per_b;
+    const size_t off = static_cast<size_t>(b) * M + static_cast<size_t>(rem / nblk3) * a.L2L3 + (rem % nblk3) * kNcol;
+    const uint32_t lo32 = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(off));
+    const uint32_t hi32 = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(off >> 32));
+    return a.buf + ((static_cast<size_t>(hi32) << 32) | lo32);
+  };
+  auto col = [](int r, int cc) { return r * kNcol + cc; };
+  // per-lane byte offset of (row tj, column c) from a tile origin; row u*TPC
+  // of the tile is a uniform (SGPR) base: one VGPR addresses all 16 accesses
+  const uint32_t lane_off = (static_cast<uint32_t>(tj) * a.L3 + c) * sizeof(float2);
+  const size_t row_step = static_cast<size_t>(TPC) * a.L3;
+  auto at = [&](const float2* origin, int u) -> const float2* {
+    return reinterpret_cast<const float2*>(reinterpret_cast<const char*>(origin + u * row_step) + lane_off);
+  };
+
+  float2 pre[16];
+  uint32_t tile = blockIdx.x;
+  if (tile < ntiles) {
+    const float2* src = tile_base(tile);
+#pragma unroll
+    for (int u = 0; u < 16; ++u) pre[u] = *at(src, u);
+  }
+  {
+    for (int e = threadIdx.x; e < L; e += NT) wl[e] = a.tb.st2[e + (e >> 4)];
+  }
+  __syncthreads();
+  while (tile < ntiles) {
+    const uint32_t b = __builtin_amdgcn_readfirstlane(tile / per_b);
+    const uint32_t rem = __builtin_amdgcn_readfirstlane(tile % per_b);
+    const uint32_t k1 = __builtin_amdgcn_readfirstlane(rem / nblk3);
+    const uint32_t n3 = (rem % nblk3) * kNcol + c;
+    float2* base = const_cast<float2*>(tile_base(tile));
+    const float2 wc = a.tb.p2col[k1 * a.L3 + n3];
+    // stage 1 (radix R1, no twiddles) on the loaded rows: butterfly
+    // j = tj + R1 v holds rows j + 16 q = tj + TPC (v + NB1 q)
+#pragma unroll
+    for (int v = 0; v < NB1; ++v) {
+      float2 x[R1];
+#pragma unroll
+      for (int q = 0; q < R1; ++q) x[q] = pre[v + NB1 * q];
+      Dft<R1>::run(x);
+      const int j = tj + R1 * v;
+#pragma unroll
+      for (int q = 0; q < R1; ++q) data[col(R1 * j + q, c)] = x[q];
+    }
+    const uint32_t next = tile + gridDim.x;
+    if (next < ntiles) {  // in flight during the exchange, stage 2 and the stores
+      const float2* src = tile_base(next);
+#pragma unroll
+      for (int u = 0; u < 16; ++u) pre[u] = *at(src, u);
+    }
+    __syncthreads();
+    // stage 2 (radix 16, Ns = R1): butterfly tj reads rows tj + R1 q, twiddle W_L^{tj q}
+    float2 y[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) y[q] = data[col(tj + R1 * q, c)];
+    __syncthreads();  // LDS tile free for the next tile's stage 1
+#pragma unroll
+    for (int q = 1; q < 16; ++q) y[q] = cmul(y[q], wl[(tj * q) % L]);
+    Dft<16>::run(y);
+    // outputs k2 = tj + TPC q
+    auto wexact = [&](uint32_t e) { return cmul(hi[e >> kP2LoBits], lo[e & (kLo - 1)]); };
+    const float2 step = wexact(n3 * static_cast<uint32_t>(TPC));
+    float2 t0 = cmul(wc, wexact(n3 * static_cast<uint32_t>(tj)));
+    float2 t8 = cmul(wc, wexact(n3 * static_cast<uint32_t>(tj + 8 * TPC)));
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      *const_cast<float2*>(at(base, q)) = cmul(y[q], t0);
+      *const_cast<float2*>(at(base, q + 8)) = cmul(y[q + 8], t8);
+      t0 = cmul(t0, step);
+      t8 = cmul(t8, step);
+    }
+    if (a.partials != nullptr && rem == 0) {
+      // mean-padding correction of template b, reduced once in a fixed order
+      const double* pp = a.partials + static_cast<size_t>(b) * a.n_partials;
+      double part = 0.0;
+      for (uint32_t i = threadIdx.x; i < a.n_partials; i += NT) part += pp[i];
+      const double tot = block_sum<NT>(part, red);
+      if (threadIdx.x == 0) {
+        const uint32_t n_s = a.tmpl[b].n_steps;
+        a.delta[b] = n_s ? tot / static_cast<double>(n_s) : 0.0;
+      }
+    }
     tile = next;
   }
 }
@@ -498,6 +720,17 @@ bool pass3_length_supported(uint32_t L) {
 
 hipError_t launch_pass1(const FFTPlan3& plan, Pass1Mode mode, const Pass1Args& a, int batch, hipStream_t s) {
   const dim3 grid(plan.wg1(), batch);
+  // padding >= 3x: every template's rows n1 >= L1/3 are zero (n_steps <= n_unpadded)
+  const bool pad3 = mode == P1_RESAMPLE && !plan.legacy_pass1 && plan.L1 % 3 == 0 &&
+                    2ull * (plan.L1 / 3) * a.L2L3 >= a.n_unpadded;
+  if (pad3 && plan.L1 == 192) {
+    hipLaunchKernelGGL((pass1_pruned3_kernel<4>), grid, dim3(kNcol * 16), 0, s, a);
+    return hipGetLastError();
+  }
+  if (pad3 && plan.L1 == 96) {
+    hipLaunchKernelGGL((pass1_pruned3_kernel<2>), grid, dim3(kNcol * 16), 0, s, a);
+    return hipGetLastError();
+  }
   switch (plan.L1) {
 #define X(n)                                                                                          \
   case n: {                                                                                           \
@@ -517,6 +750,17 @@ hipError_t launch_pass1(const FFTPlan3& plan, Pass1Mode mode, const Pass1Args& a
 hipError_t launch_pass2(const FFTPlan3& plan, const Pass2Args& a, int batch, hipStream_t s) {
   const uint32_t ntiles = plan.wg2() * static_cast<uint32_t>(batch);
   const dim3 grid(plan.persist_wgs ? std::min(ntiles, plan.persist_wgs) : ntiles);
+  if (!plan.legacy_pass2) {
+    switch (plan.L2) {
+#define X(n)                                                                                   \
+  case n:                                                                                      \
+    hipLaunchKernelGGL((pass2r_kernel<n>), grid, dim3(kNcol * (n / 16)), 0, s, a, ntiles);     \
+    return hipGetLastError();
+      X(32) X(64) X(128) X(256)
+#undef X
+      default: break;
+    }
+  }
   switch (plan.L2) {
 #define X(n)                                                                \
   case n:                                                                   \
