@@ -22,6 +22,7 @@
 #include "../core/cpu_backend.hpp"
 #include "../core/log.hpp"
 #include "../core/rngmed.hpp"
+#include "../hip/fft2_kernels.hpp"
 #include "../hip/fft_kernels.hpp"
 #include "../hip/hs_kernels.hpp"
 #include "../hip/resample_kernels.hpp"
@@ -156,9 +157,13 @@ struct HipEngine::Impl {
   bool ready = false;
   uint32_t num_cus = 256;
   bool ps_fp16 = false;         // config 5: fp16 power spectrum between pass 3 and the harmonic sum
+  bool hs_gather = std::getenv("BRP_HS_STAGED") == nullptr;  // LDS-staged segments only on request (measured slower)
   uint32_t persist_per_cu = 4;  // persistent FFT passes: workgroups per CU (BRP_PERSIST, 0 = off)
   uint32_t ps_stride = 0;
   uint32_t i_start = 0;
+  // two-pass template FFT (fft2.hip) for the 3x-padded production shape
+  // M = 768 * 8192; the three-pass plan stays in use for whitening
+  bool two_pass = false;
 
   DevBuf<float> series;
   DevBuf<float2> buf;           // [batch][M]
@@ -174,6 +179,8 @@ struct HipEngine::Impl {
   DevBuf<float2> w_spec, w_z;   // whitening scratch: half spectrum, packed inverse input
   DevBuf<float> w_psw, w_med;   // whitening scratch: power spectrum, running median
   DevBuf<float2> t_st1, t_st2, t_st3, t_p1, t_p2col, t_p2lo, t_p2hi, t_p3;
+  DevBuf<float2> t_w768, t_t256, t_t4096, t_t8192;  // two-pass tables
+  DevBuf<float> pss;            // [batch][M] slab-major power spectrum (two-pass)
 
   PinnedBuf<uint8_t> h_in;
   struct { TemplateDev* p = nullptr; } h_tmpl;
@@ -233,7 +240,24 @@ struct HipEngine::Impl {
     v.assign(32 + 4ull * L3 / 32, make_float2(0, 0));
     for (uint32_t i = 0; i < 32; ++i) v[i] = root(i, 4ull * L3);
     for (uint32_t m = 0; m < 4 * L3 / 32; ++m) v[32 + m] = root(32ull * m, 4ull * L3);
-    return upload(t_p3, v);
+    if ((rc = upload(t_p3, v))) return rc;
+    if (!two_pass) return 0;
+    v.assign(hipk::kFft2L1, make_float2(0, 0));
+    for (uint32_t e = 0; e < hipk::kFft2L1; ++e) v[e] = root(e, hipk::kFft2L1);
+    if ((rc = upload(t_w768, v))) return rc;
+    v.assign(256, make_float2(0, 0));
+    for (uint32_t e = 0; e < 256; ++e) v[e] = root(e, 256);
+    if ((rc = upload(t_t256, v))) return rc;
+    // two-level W_4096 / W_8192: lo[e & 63] * hi[e >> 6]
+    for (uint32_t n : {4096u, 8192u}) {
+      v.assign(128, make_float2(0, 0));
+      for (uint32_t e = 0; e < 64; ++e) {
+        v[e] = root(e, n);
+        v[64 + e] = root(64ull * e, n);
+      }
+      if ((rc = upload(n == 4096 ? t_t4096 : t_t8192, v))) return rc;
+    }
+    return 0;
   }
 
   hipk::TwiddleTable twt() const {
@@ -263,6 +287,18 @@ struct HipEngine::Impl {
         if (e != hipSuccess) return e;
         return hipk::launch_nsteps(tmpl.p, nb, stream, &cands.p[0].x);
       case kPass1: {
+        if (two_pass) {
+          hipk::ColAArgs aa{};
+          aa.out = buf.p;
+          aa.M = plan.M;
+          aa.series = series.p;
+          aa.n_unpadded = g.n_unpadded;
+          aa.tmpl = tmpl.p;
+          aa.partials = partials.p;
+          aa.tw = tw;
+          aa.w768 = t_w768.p;
+          return hipk::launch_colA(aa, nb, stream);
+        }
         hipk::Pass1Args a1{};
         a1.out = buf.p;
         a1.L2L3 = plan.L2 * plan.L3;
@@ -276,6 +312,26 @@ struct HipEngine::Impl {
         return hipk::launch_pass1(plan, hipk::P1_RESAMPLE, a1, nb, stream);
       }
       case kPass2: {
+        if (two_pass) {
+          hipk::RowBArgs ab{};
+          ab.buf = buf.p;
+          ab.M = plan.M;
+          ab.tw = tw;
+          ab.t256 = t_t256.p;
+          ab.t4096 = t_t4096.p;
+          ab.t8192 = t_t8192.p;
+          ab.limit = std::min(g.harmonic_idx_hi, g.fft_size);
+          ab.pss = pss.p;
+          ab.pss_stride = plan.M;
+          ab.norm = static_cast<float>(1.0 / g.nsamples);
+          ab.tmpl = tmpl.p;
+          ab.partials = partials.p;
+          ab.n_partials = hipk::kFft2R / 16;
+          ab.ps = ps.p;
+          ab.ps16 = ps_fp16 ? reinterpret_cast<_Float16*>(ps.p) : nullptr;
+          ab.ps_stride = ps_stride;
+          return hipk::launch_rowB(ab, nb, stream);
+        }
         hipk::Pass2Args a2{};
         a2.buf = buf.p;
         a2.L1 = plan.L1;
@@ -290,6 +346,17 @@ struct HipEngine::Impl {
         return hipk::launch_pass2(plan, a2, nb, stream);
       }
       case kPass3: {
+        if (two_pass) {
+          hipk::PsTArgs at{};
+          at.pss = pss.p;
+          at.pss_stride = plan.M;
+          at.ps = ps.p;
+          at.ps16 = ps_fp16 ? reinterpret_cast<_Float16*>(ps.p) : nullptr;
+          at.ps_stride = ps_stride;
+          at.limit = std::min(g.harmonic_idx_hi, g.fft_size);
+          at.M = plan.M;
+          return hipk::launch_psT(at, nb, stream);
+        }
         hipk::Pass3Args a3{};
         a3.buf = buf.p;
         a3.L1 = plan.L1;
@@ -320,6 +387,7 @@ struct HipEngine::Impl {
         ah.thr = thr.p;
         ah.list = cands.p;
         ah.cap = cap;
+        ah.gather = hs_gather;
         return hipk::launch_harmonic_sum(ah, nb, stream);
       }
       case kEpilogue:
@@ -406,6 +474,10 @@ int HipEngine::setup(const SearchGeometry& g, const std::vector<float>& series, 
   }
   if (const char* e = std::getenv("BRP_PERSIST")) d.persist_per_cu = static_cast<uint32_t>(std::atoi(e));
   d.plan.persist_wgs = d.persist_per_cu * d.num_cus;
+  // opt-in (BRP_FFT2=1): measured 84 vs 78 us/template sequential, the
+  // three-pass kernels keep more workgroups per CU (profiles/README.md)
+  d.two_pass = d.plan.M == hipk::kFft2M && 2ull * (hipk::kFft2L1 / 3) * hipk::kFft2R >= g.n_unpadded &&
+               std::getenv("BRP_FFT2") != nullptr;
   d.plan.legacy_pass1 = std::getenv("BRP_P1_LEGACY") != nullptr;
   d.plan.legacy_pass2 = std::getenv("BRP_P2_LEGACY") != nullptr;
   log_message(LOG_DEBUG, true, "FFT plan: N=%u M=%u = %u x %u x %u\n", g.nsamples, d.plan.M, d.plan.L1, d.plan.L2,
@@ -420,7 +492,12 @@ int HipEngine::setup(const SearchGeometry& g, const std::vector<float>& series, 
   if ((rc = d.buf.alloc(B * d.plan.M))) return rc;
   // + slack: the harmonic-sum staging copies whole 64-float chunks past the last bin
   if ((rc = d.ps.alloc(B * d.ps_stride + 1024))) return rc;
-  if ((rc = d.partials.alloc(B * d.plan.wg1()))) return rc;
+  if ((rc = d.partials.alloc(B * std::max<size_t>(d.plan.wg1(), hipk::kFft2R / 16)))) return rc;
+  if (d.two_pass) {
+    if ((rc = d.pss.alloc(B * d.plan.M))) return rc;
+  } else {
+    d.pss.release();
+  }
   if ((rc = d.delta.alloc(B))) return rc;
   if (B > hipk::kHsMaxBatch || g.fundamental_idx_hi >= (1u << hipk::kHsBinBits)) {
     log_message(LOG_ERROR, true, "Batch %zu / fundamental_idx_hi %u beyond the candidate key packing.\n", B,
@@ -727,6 +804,55 @@ int HipEngine::power_spectrum(const TemplateInput& t, std::vector<float>& ps_out
                 RADPUL_HIP_MEM_COPY_HOST_DEVICE);
   BRP_HIP_CHECK(hipk::launch_nsteps(d.tmpl.p, 1, s), RADPUL_HIP_KERNEL_INVOKE);
   const hipk::TwiddleTable tw = d.twt();
+  if (d.two_pass) {
+    // the template pipeline's transform: pass A, pass B, transpose (all bins)
+    DevBuf<float> full;
+    int rc;
+    if ((rc = full.alloc(g.fft_size))) return rc;
+    hipk::ColAArgs aa{};
+    aa.out = d.buf.p;
+    aa.M = d.plan.M;
+    aa.series = d.series.p;
+    aa.n_unpadded = g.n_unpadded;
+    aa.tmpl = d.tmpl.p;
+    aa.partials = d.partials.p;
+    aa.tw = tw;
+    aa.w768 = d.t_w768.p;
+    BRP_HIP_CHECK(hipk::launch_colA(aa, 1, s), RADPUL_HIP_KERNEL_INVOKE);
+    hipk::RowBArgs ab{};
+    ab.buf = d.buf.p;
+    ab.M = d.plan.M;
+    ab.tw = tw;
+    ab.t256 = d.t_t256.p;
+    ab.t4096 = d.t_t4096.p;
+    ab.t8192 = d.t_t8192.p;
+    ab.limit = g.fft_size;
+    ab.pss = d.pss.p;
+    ab.pss_stride = d.plan.M;
+    ab.norm = static_cast<float>(1.0 / g.nsamples);
+    ab.tmpl = d.tmpl.p;
+    ab.partials = d.partials.p;
+    ab.n_partials = hipk::kFft2R / 16;
+    ab.ps = full.p;
+    ab.ps_stride = g.fft_size;
+    BRP_HIP_CHECK(hipk::launch_rowB(ab, 1, s), RADPUL_HIP_KERNEL_INVOKE);
+    hipk::PsTArgs at{};
+    at.pss = d.pss.p;
+    at.pss_stride = d.plan.M;
+    at.ps = full.p;
+    at.ps_stride = g.fft_size;
+    at.limit = g.fft_size;
+    at.M = d.plan.M;
+    BRP_HIP_CHECK(hipk::launch_psT(at, 1, s), RADPUL_HIP_KERNEL_INVOKE);
+    ps_out.resize(g.fft_size);
+    BRP_HIP_CHECK(hipMemcpyAsync(ps_out.data(), full.p, g.fft_size * sizeof(float), hipMemcpyDeviceToHost, s),
+                  RADPUL_HIP_MEM_COPY_DEVICE_HOST);
+    BRP_HIP_CHECK(hipMemcpyAsync(d.h_tmpl.p, d.tmpl.p, sizeof(TemplateDev), hipMemcpyDeviceToHost, s),
+                  RADPUL_HIP_MEM_COPY_DEVICE_HOST);
+    BRP_HIP_CHECK(hipStreamSynchronize(s), RADPUL_HIP_KERNEL_INVOKE);
+    if (n_steps) *n_steps = d.h_tmpl.p[0].n_steps;
+    return 0;
+  }
   hipk::Pass1Args a1{};
   a1.out = d.buf.p;
   a1.L2L3 = d.plan.L2 * d.plan.L3;

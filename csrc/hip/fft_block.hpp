@@ -303,7 +303,61 @@ struct BlockFFT {
   static __device__ __forceinline__ void run_pruned(float2* lds, const float2* tw) {
     Radices<L>::template apply<ImplPruned>::run(lds, tw);
   }
+  // stages 2.. only: the caller has done stage 1 (radix kFirstRadix, Ns = 1)
+  // in registers and written its Stockham output to LDS
+  template <int R0, int... Rs>
+  struct ImplRest {
+    static __device__ __forceinline__ void run(float2* lds, const float2* tw) {
+      BlockStages<L, NCOL, TPC, ROWMAJOR, R0, Rs...>::run(lds, tw);
+    }
+  };
+  static __device__ __forceinline__ void run_rest(float2* lds, const float2* tw) {
+    Radices<L>::template apply<ImplRest>::run(lds, tw);
+  }
 };
+
+// ------------------------------------------------------------ shared helpers
+// block-wide deterministic sum of one double per thread (result valid in all threads)
+template <int NT>
+__device__ __forceinline__ double block_sum(double v, double* scratch) {
+  v = wave_sum(v);
+  const int w = threadIdx.x / kWave;
+  constexpr int kWaves = (NT + kWave - 1) / kWave;
+  __syncthreads();
+  if ((threadIdx.x % kWave) == 0) scratch[w] = v;
+  __syncthreads();
+  double t = 0.0;
+#pragma unroll
+  for (int i = 0; i < kWaves; ++i) t += scratch[i];
+  __syncthreads();
+  return t;
+}
+
+// X_k of the real FFT from Z_k, Z_{M-k} of the packed complex FFT and w = W_N^k.
+__device__ __forceinline__ float2 untangle_w(float2 zk, float2 zmk, float2 w) {
+  const float2 bc = conjf2(zmk);
+  const float2 e = cscale(cadd(zk, bc), 0.5f);
+  const float2 o = cscale(csub(zk, bc), 0.5f);
+  return cadd(e, mul_mi(cmul(w, o)));
+}
+
+// FFT of the padding indicator 1[m >= n_s] (m < N) at bin k in [1, N/2]:
+// S_k = -(sin(pi n_s k / N) / sin(pi k / N)) * exp(-i pi (n_s - 1) k / N),
+// from ta = W_2N^{n_s k}, tk = W_2N^k, tc = W_2N^{(n_s-1) k}.
+__device__ __forceinline__ float2 padding_spectrum_t(float2 ta, float2 tk, float2 tc) {
+  const float ratio = ta.y / tk.y;
+  return make_float2(-ratio * tc.x, -ratio * tc.y);
+}
+
+// multiply by (-i)^q
+__device__ __forceinline__ float2 rot_mi(float2 a, uint32_t q) {
+  switch (q & 3u) {
+    case 0: return a;
+    case 1: return make_float2(a.y, -a.x);
+    case 2: return make_float2(-a.x, -a.y);
+    default: return make_float2(-a.y, a.x);
+  }
+}
 
 // Stage twiddle table W_L^e (e < L) stored at e + e/16 (kTwPad<L> entries) so the
 // stride-q reads of a radix-16 stage do not collide on LDS banks. The host

@@ -26,24 +26,6 @@ constexpr int tpc_for() {
   return (L / 16) < 1 ? 1 : (L / 16);
 }
 
-// block-wide deterministic sum of one double per thread (result valid in all threads)
-template <int NT>
-__device__ __forceinline__ double block_sum(double v, double* scratch) {
-  v = wave_sum(v);
-  const int w = threadIdx.x / kWave;
-  constexpr int kWaves = (NT + kWave - 1) / kWave;
-  __syncthreads();
-  if ((threadIdx.x % kWave) == 0) scratch[w] = v;
-  __syncthreads();
-  double t = 0.0;
-#pragma unroll
-  for (int i = 0; i < kWaves; ++i) t += scratch[i];
-  __syncthreads();
-  return t;
-}
-
-
-
 // ------------------------------------------------------------------ pass 1
 template <int L, int MODE>
 __global__ void __launch_bounds__(kNcol * tpc_for<L>()) pass1_kernel(Pass1Args a) {
@@ -477,22 +459,6 @@ __device__ __forceinline__ size_t row_base(uint32_t c, uint32_t L1, uint32_t L2,
   return (static_cast<size_t>(k1) * L2 + k2) * L3;
 }
 
-// X_k of the real FFT from Z_k, Z_{M-k} of the packed complex FFT and w = W_N^k.
-__device__ __forceinline__ float2 untangle_w(float2 zk, float2 zmk, float2 w) {
-  const float2 bc = conjf2(zmk);
-  const float2 e = cscale(cadd(zk, bc), 0.5f);
-  const float2 o = cscale(csub(zk, bc), 0.5f);
-  return cadd(e, mul_mi(cmul(w, o)));
-}
-
-// FFT of the padding indicator 1[m >= n_s] (m < N) at bin k in [1, N/2]:
-// S_k = -(sin(pi n_s k / N) / sin(pi k / N)) * exp(-i pi (n_s - 1) k / N),
-// from ta = W_2N^{n_s k}, tk = W_2N^k, tc = W_2N^{(n_s-1) k}.
-__device__ __forceinline__ float2 padding_spectrum_t(float2 ta, float2 tk, float2 tc) {
-  const float ratio = ta.y / tk.y;
-  return make_float2(-ratio * tc.x, -ratio * tc.y);
-}
-
 __device__ __forceinline__ float2 padding_spectrum(const TwiddleTable& tw, uint32_t n_s, uint32_t k) {
   return padding_spectrum_t(tw_lookup(tw, static_cast<uint64_t>(n_s) * k), tw_lookup32(tw, k),
                             tw_lookup(tw, static_cast<uint64_t>(n_s - 1) * k));
@@ -509,16 +475,6 @@ __device__ __forceinline__ RowTw row_twiddles(const TwiddleTable& tw, uint32_t c
   r.t1 = tw_lookup32(tw, c);
   r.ta = tw_lookup(tw, static_cast<uint64_t>(n_s) * c);
   return r;
-}
-
-// multiply by (-i)^q
-__device__ __forceinline__ float2 rot_mi(float2 a, uint32_t q) {
-  switch (q & 3u) {
-    case 0: return a;
-    case 1: return make_float2(a.y, -a.x);
-    case 2: return make_float2(-a.x, -a.y);
-    default: return make_float2(-a.y, a.x);
-  }
 }
 
 template <int L, int ROWS, int MODE>
@@ -544,7 +500,17 @@ __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Arg
   // lines: keep them on one XCD so its L2 merges full lines
   const uint32_t c0 = xcd_remap(blockIdx.x, gridDim.x) * ROWS;
 
-  {
+  // stage 1 (radix R0, Ns = 1) straight from global memory: butterfly
+  // j = tj + TPC u reads elements j + (L/R0) q of its row (lanes walk j:
+  // contiguous 8-B loads), transforms in registers and writes its Stockham
+  // output rows R0 j + q to LDS; the remaining stages run LDS -> LDS
+  constexpr int R0 = BlockFFT<L, NSLOT, TPC, true>::kFirstRadix;
+  constexpr int kBf0 = L / R0;
+  // Measured on MI355X (L = 256): 16-B row loads into LDS beat the 8-B loads
+  // the register first stage needs (18.2 vs 18.9 us/template), so the
+  // register path is kept for reference but disabled.
+  constexpr bool kRegStage1 = false && (kBf0 % TPC == 0);
+  if constexpr (!kRegStage1) {
     int slot, tj;
     Lay::coords(threadIdx.x, slot, tj);
     const uint32_t cs = c0 + (slot % ROWS);
@@ -554,6 +520,24 @@ __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Arg
       const float4 v = src[r];
       data[Lay::idx(2 * r, slot)] = make_float2(v.x, v.y);
       data[Lay::idx(2 * r + 1, slot)] = make_float2(v.z, v.w);
+    }
+  } else {
+    int slot, tj;
+    Lay::coords(threadIdx.x, slot, tj);
+    const uint32_t cs = c0 + (slot % ROWS);
+    const uint32_t row = (slot < ROWS) ? cs : (a.C - cs) % a.C;
+    const float2* src = buf + row_base(row < a.C ? row : 0, a.L1, a.L2, a.L3);
+    float2 v[kBf0 / TPC][R0];
+#pragma unroll
+    for (int u = 0; u < kBf0 / TPC; ++u)
+#pragma unroll
+      for (int q = 0; q < R0; ++q) v[u][q] = src[tj + u * TPC + q * kBf0];
+#pragma unroll
+    for (int u = 0; u < kBf0 / TPC; ++u) {
+      Dft<R0>::run(v[u]);
+      const int j = tj + u * TPC;
+#pragma unroll
+      for (int q = 0; q < R0; ++q) data[Lay::idx(R0 * j + q, slot)] = v[u][q];
     }
   }
   copy_stage_twiddles<L>(twl, a.tb.st3);
@@ -576,7 +560,8 @@ __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Arg
   const uint32_t half = a.C / 2;
   const RowTw rt = row_twiddles(a.tw, c, n_s);
   __syncthreads();
-  BlockFFT<L, NSLOT, TPC, true>::run(data, twl);
+  if constexpr (kRegStage1) BlockFFT<L, NSLOT, TPC, true>::run_rest(data, twl);
+  else BlockFFT<L, NSLOT, TPC, true>::run(data, twl);
 
   const float dS = static_cast<float>(delta);
   constexpr bool kPower = (MODE == P3_POWER || MODE == P3_POWER16);

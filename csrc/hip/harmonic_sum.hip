@@ -14,6 +14,8 @@
 // dirty-page flags that the host then scans, each workgroup appends only the
 // (bin, power) pairs above the device threshold to per-level candidate lists
 // (wave-aggregated atomics); the host merges them into the candidate table.
+#include <type_traits>
+
 #include "hip_common.hpp"
 #include "hs_kernels.hpp"
 
@@ -44,50 +46,142 @@ __device__ __forceinline__ void emit(uint32_t* counter, uint2* list, uint32_t ca
   }
 }
 
+// LDS staging of the harmonic segments: for harmonic l the tile's bins
+// (l*i + 8) >> 4, i in [i0, i0 + kSpan), form one contiguous run of about
+// l*kSpan/16 bins. All 16 runs (8.5 bins per i in total) are copied into LDS
+// with 16-B loads, so the 16 per-i gathers become LDS reads (conflict free:
+// the lanes of a wave read at most 4l consecutive words). The run of harmonic
+// l starts at the 4-aligned bin lo4(l) and occupies kStageCap(l) floats.
+__host__ __device__ constexpr int stage_cap(int l) { return ((l * (kSpan - 1) / 16 + 5 + 3) / 4) * 4; }
+__host__ __device__ constexpr int stage_off(int l) { return l <= 1 ? 0 : stage_off(l - 1) + stage_cap(l - 1); }
+constexpr int kStageFloats = stage_off(17);
+// per harmonic l: ceil(chunks / threads) load iterations
+__host__ __device__ constexpr int stage_iters(int l) { return (stage_cap(l) / 4 + kThreads - 1) / kThreads; }
+__host__ __device__ constexpr int stage_iters_before(int l) { return l <= 1 ? 0 : stage_iters_before(l - 1) + stage_iters(l - 1); }
+__host__ __device__ constexpr int stage_iters_total() { return stage_iters_before(17); }
+
+// f(integral_constant<l>, integral_constant<it>, flat iteration base) for
+// l = 1..16 and it < stage_iters(l), fully unrolled
+template <int L, int IT, typename F>
+__device__ __forceinline__ void stage_for_each_impl(F&& f) {
+  if constexpr (L <= 16) {
+    if constexpr (IT < stage_iters(L)) {
+      f(std::integral_constant<int, L>{}, std::integral_constant<int, IT>{}, stage_iters_before(L));
+      stage_for_each_impl<L, IT + 1>(f);
+    } else {
+      stage_for_each_impl<L + 1, 0>(f);
+    }
+  }
+}
+template <typename F>
+__device__ __forceinline__ void stage_for_each(F&& f) {
+  stage_for_each_impl<1, 0>(f);
+}
+static_assert(kStageFloats >= 4 * kSpanPad, "S_1..S_4 alias the staging area");
+
 // T = float (exact path) or _Float16 (config 5 spectrum); every element is
-// widened to float before the reference-order float sums
-template <typename T>
+// widened to float before the reference-order float sums. STAGED: harmonic
+// segments staged in LDS (default) or gathered per i from global memory.
+template <typename T, bool STAGED>
 __global__ void __launch_bounds__(kThreads) harmonic_sum_kernel(HSArgs a) {
 #pragma clang fp contract(off)
-  __shared__ __attribute__((aligned(16))) float sv[4][kSpanPad];  // S_1..S_4 over the tile + halo
+  // staged segments, then (after a barrier) S_1..S_4 over the tile + halo
+  __shared__ __attribute__((aligned(16))) float lds[STAGED ? kStageFloats : 4 * kSpanPad];
+  float (*sv)[kSpanPad] = reinterpret_cast<float (*)[kSpanPad]>(lds);
   const int b = blockIdx.y;
   const T* P = reinterpret_cast<const T*>(sizeof(T) == 4 ? static_cast<const void*>(a.ps)
                                                         : static_cast<const void*>(a.ps16)) +
                static_cast<size_t>(b) * a.ps_stride;
-  auto ld = [&](uint32_t idx) { return static_cast<float>(P[idx]); };
   const uint32_t i0 = a.i_start + blockIdx.x * kHsTile;
   const float ninf = -__builtin_inff();
+  auto lo4 = [&](uint32_t l) { return ((l * i0 + 8u) >> 4) & ~3u; };
 
-  for (int t = threadIdx.x; t < kSpan; t += kThreads) {
+  if (STAGED) {
+    // harmonic by harmonic (compile-time l: the run's origin is a scalar and
+    // no per-lane selection is needed); every load is issued before the first
+    // LDS write. Chunks past the spectrum's stride read as zero (only i >= hhi
+    // would use them).
+    constexpr int kIters = stage_iters_total();
+    float4 v[kIters];
+    stage_for_each([&](auto l_tag, auto it_tag, int it_base) {
+      constexpr int l = decltype(l_tag)::value;
+      constexpr int it = decltype(it_tag)::value;
+      constexpr int nch = stage_cap(l) / 4;
+      const int ch = static_cast<int>(threadIdx.x) + it * kThreads;
+      v[it_base + it] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (ch < nch) {
+        const uint32_t bin = lo4(l) + 4u * static_cast<uint32_t>(ch);
+        if (bin + 4 <= a.ps_stride) {
+          if constexpr (sizeof(T) == 4) {
+            v[it_base + it] = *reinterpret_cast<const float4*>(P + bin);
+          } else {
+            const uint2 h = *reinterpret_cast<const uint2*>(P + bin);
+            const _Float16* hh = reinterpret_cast<const _Float16*>(&h);
+            v[it_base + it] = make_float4(static_cast<float>(hh[0]), static_cast<float>(hh[1]),
+                                          static_cast<float>(hh[2]), static_cast<float>(hh[3]));
+          }
+        }
+      }
+    });
+    stage_for_each([&](auto l_tag, auto it_tag, int it_base) {
+      constexpr int l = decltype(l_tag)::value;
+      constexpr int it = decltype(it_tag)::value;
+      const int ch = static_cast<int>(threadIdx.x) + it * kThreads;
+      if (ch < stage_cap(l) / 4) reinterpret_cast<float4*>(lds + stage_off(l))[ch] = v[it_base + it];
+    });
+    __syncthreads();
+  }
+  auto ld = [&](uint32_t l, uint32_t i) -> float {
+    const uint32_t bin = (l * i + 8u) >> 4;
+    if (STAGED) return lds[stage_off(static_cast<int>(l)) + static_cast<int>(bin - lo4(l))];
+    return static_cast<float>(P[bin]);
+  };
+
+  constexpr int kIt = (kSpan + kThreads - 1) / kThreads;
+  float s1[kIt], s2[kIt], s3[kIt], s4[kIt], p0[kIt];
+#pragma unroll
+  for (int it = 0; it < kIt; ++it) {
+    const int t = threadIdx.x + it * kThreads;
     const uint32_t i = i0 + t;
-    float s1 = ninf, s2 = ninf, s3 = ninf, s4 = ninf;
-    if (i >= a.w2 && i < a.hhi) {
-      float sum = ld(i);
-      sum += ld((8u * i + 8u) >> 4);
-      s1 = sum;
-      sum += ld((12u * i + 8u) >> 4) + ld((4u * i + 8u) >> 4);
-      s2 = sum;
-      sum += ld((14u * i + 8u) >> 4) + ld((10u * i + 8u) >> 4) + ld((6u * i + 8u) >> 4) + ld((2u * i + 8u) >> 4);
-      s3 = sum;
-      sum += ld((15u * i + 8u) >> 4) + ld((13u * i + 8u) >> 4) + ld((11u * i + 8u) >> 4) + ld((9u * i + 8u) >> 4) +
-             ld((7u * i + 8u) >> 4) + ld((5u * i + 8u) >> 4) + ld((3u * i + 8u) >> 4) + ld((i + 8u) >> 4);
-      s4 = sum;
+    s1[it] = s2[it] = s3[it] = s4[it] = ninf;
+    p0[it] = 0.0f;
+    if (t < kSpan && i >= a.w2 && i < a.hhi) {
+      float sum = ld(16, i);
+      p0[it] = sum;
+      sum += ld(8, i);
+      s1[it] = sum;
+      sum += ld(12, i) + ld(4, i);
+      s2[it] = sum;
+      sum += ld(14, i) + ld(10, i) + ld(6, i) + ld(2, i);
+      s3[it] = sum;
+      sum += ld(15, i) + ld(13, i) + ld(11, i) + ld(9, i) + ld(7, i) + ld(5, i) + ld(3, i) + ld(1, i);
+      s4[it] = sum;
     }
-    sv[0][sidx(t)] = s1;
-    sv[1][sidx(t)] = s2;
-    sv[2][sidx(t)] = s3;
-    sv[3][sidx(t)] = s4;
+  }
+  if (STAGED) __syncthreads();  // staging area becomes sv
+#pragma unroll
+  for (int it = 0; it < kIt; ++it) {
+    const int t = threadIdx.x + it * kThreads;
+    if (t < kSpan) {
+      sv[0][sidx(t)] = s1[it];
+      sv[1][sidx(t)] = s2[it];
+      sv[2][sidx(t)] = s3[it];
+      sv[3][sidx(t)] = s4[it];
+    }
   }
   __syncthreads();
 
   uint32_t* count = &a.list[0].x;
   uint2* list = a.list + 1;
   const float thr0 = a.thr[static_cast<size_t>(b) * kHsThrStride + 0];
-  // level 0: the power spectrum itself
-  for (int t = threadIdx.x; t < kHsTile; t += kThreads) {
+  // level 0: the power spectrum itself (kept in registers from the S_1 sums)
+#pragma unroll
+  for (int it = 0; it < kIt; ++it) {
+    const int t = threadIdx.x + it * kThreads;
+    if (t - static_cast<int>(threadIdx.x) >= kHsTile) break;  // uniform: whole iterations past the tile
     const uint32_t i = i0 + t;
-    const bool in = (i >= a.w2 && i < a.fhi);
-    const float p = in ? ld(i) : 0.0f;
+    const bool in = t < kHsTile && (i >= a.w2 && i < a.fhi);
+    const float p = in ? p0[it] : 0.0f;
     emit(count, list, a.cap, in && p > thr0, hs_pack(b, 0, i), p);
   }
   // levels 1..4: group of 2^h consecutive i starting at s == 2^(h-1) mod 2^h;
@@ -129,10 +223,14 @@ uint32_t hs_num_tiles(uint32_t i_start, uint32_t hhi) {
 hipError_t launch_harmonic_sum(const HSArgs& a, int batch, hipStream_t s) {
   const uint32_t tiles = hs_num_tiles(a.i_start, a.hhi);
   if (tiles == 0) return hipSuccess;
-  if (a.ps16 != nullptr)
-    hipLaunchKernelGGL(harmonic_sum_kernel<_Float16>, dim3(tiles, batch), dim3(kThreads), 0, s, a);
-  else
-    hipLaunchKernelGGL(harmonic_sum_kernel<float>, dim3(tiles, batch), dim3(kThreads), 0, s, a);
+  const dim3 grid(tiles, batch);
+  if (a.gather) {
+    if (a.ps16 != nullptr) hipLaunchKernelGGL((harmonic_sum_kernel<_Float16, false>), grid, dim3(kThreads), 0, s, a);
+    else hipLaunchKernelGGL((harmonic_sum_kernel<float, false>), grid, dim3(kThreads), 0, s, a);
+  } else {
+    if (a.ps16 != nullptr) hipLaunchKernelGGL((harmonic_sum_kernel<_Float16, true>), grid, dim3(kThreads), 0, s, a);
+    else hipLaunchKernelGGL((harmonic_sum_kernel<float, true>), grid, dim3(kThreads), 0, s, a);
+  }
   return hipGetLastError();
 }
 

@@ -125,3 +125,26 @@ def test_whitening_overlapping_zaps_deterministic(brp, gpu, tmp_path):
     np.testing.assert_array_equal(w1, w2)
     rms = float(np.sqrt(np.mean(w_cpu.astype(np.float64) ** 2)))
     assert np.max(np.abs(w1 - w_cpu)) / rms < 1e-4
+
+
+def test_two_pass_fft_matches_cpu(brp, gpu, monkeypatch):
+    """Opt-in two-pass template transform (BRP_FFT2=1: 768-point gather-fused
+    column pass, 8192-point row-pair pass, slab-major transpose) on the bench
+    geometry vs the CPU golden model, and the full search table vs the default
+    three-pass path on the first templates of the bench bank."""
+    monkeypatch.setenv("BRP_FFT2", "1")
+    hdr, series, _ = brp.read_work_unit(str(WU))
+    opt = dict(OPT_BENCH, white=True)
+    geom = brp.derive_geometry(hdr, opt)
+    eng = _engine(brp, geom, series)
+    series = eng.whiten(opt, brp.read_zaplist(str(ZAP)), series)
+    P, tau, psi = brp.read_template_bank(str(BANK))
+    for k in (0, 3):
+        ps_gpu, ns_gpu = eng.power_spectrum(float(P[k]), float(tau[k]), float(psi[k]))
+        ps_cpu, ns_cpu = _cpu_ps(brp, series, geom, float(P[k]), float(tau[k]), float(psi[k]))
+        assert ns_gpu == ns_cpu
+        lim = geom["harmonic_idx_hi"]
+        scale = float(np.median(ps_cpu[geom["window_2"]:lim]))
+        err = np.abs(ps_gpu[1:lim].astype(np.float64) - ps_cpu[1:lim]) / np.maximum(ps_cpu[1:lim], scale)
+        assert np.percentile(err, 99.9) < 2e-5, (k, np.percentile(err, 99.9))
+        assert err.max() < 1e-3, (k, err.max(), int(np.argmax(err)) + 1)

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 #include "../csrc/hip/fft_block.hpp"
@@ -98,9 +99,16 @@ float time_it(F f, int reps) {
   return ms / reps;
 }
 
-int main() {
+__global__ void copy2_kernel(const float2* __restrict__ in, float2* __restrict__ out, size_t n) {
+  size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (; i < n; i += stride) out[i] = in[i];
+}
+
+int main(int argc, char** argv) {
   const size_t M = 6291456;  // complex elements of one template (50 MB)
-  const int B = 4;           // templates
+  const int B = argc > 1 ? atoi(argv[1]) : 4;  // templates (16: 800 MB, beyond the 256 MB Infinity Cache)
+  printf("buffer %d templates = %.0f MB\n", B, B * M * 8 / 1e6);
   const size_t n = M * B;
   float2 *buf, *buf2;
   CHECK(hipMalloc(&buf, n * sizeof(float2)));
@@ -111,6 +119,8 @@ int main() {
     const size_t n4 = n / 2;
     float ms = time_it([&] { hipLaunchKernelGGL(copy_kernel, dim3(4096), dim3(256), 0, 0, (const float4*)buf, (float4*)buf2, n4); }, 20);
     printf("copy float4           %8.3f ms  %6.2f TB/s\n", ms, bytes_rw / ms / 1e9);
+    ms = time_it([&] { hipLaunchKernelGGL(copy2_kernel, dim3(4096), dim3(256), 0, 0, (const float2*)buf, buf2, n); }, 20);
+    printf("copy float2           %8.3f ms  %6.2f TB/s\n", ms, bytes_rw / ms / 1e9);
   }
   // pass-2 like: L=128 rows, stride S=256 complex (2 KB), slabs = M/(128*256)
   {
