@@ -346,6 +346,23 @@ PYBIND11_MODULE(_brp, m) {
     cpu_resample(series.data(), p, out, &n_steps, &mean);
     return py::make_tuple(py::array_t<float>(out.size(), out.data()), n_steps, mean);
   });
+  // n_steps of many templates: bracketed search (what the HIP engine uploads)
+  // and the reference's descending scan
+  m.def("n_steps", [](const py::dict& gd, py::array_t<float> P, py::array_t<float> tau, py::array_t<float> psi,
+                      bool scan) {
+    const SearchGeometry g = dict_to_geometry(gd);
+    const size_t n = static_cast<size_t>(P.size());
+    py::array_t<uint32_t> out(n);
+    auto o = out.mutable_unchecked<1>();
+    auto pp = P.unchecked<1>();
+    auto tt = tau.unchecked<1>();
+    auto ss = psi.unchecked<1>();
+    for (size_t i = 0; i < n; ++i) {
+      const ResampParams p = make_resamp_params(g.nsamples, g.n_unpadded, g.fft_size, g.dt, g.step_inv, pp(i), tt(i), ss(i));
+      o(i) = scan ? resamp_n_steps_scan(p, kSinLut, kCosLut) : resamp_n_steps(p, kSinLut, kCosLut);
+    }
+    return out;
+  }, py::arg("geometry"), py::arg("P"), py::arg("tau"), py::arg("psi"), py::arg("scan") = false);
   m.def("cpu_power_spectrum", [](py::array_t<float, py::array::c_style> x, uint32_t fft_size) {
     std::vector<float> v(x.data(), x.data() + x.size()), ps;
     cpu_power_spectrum(v, fft_size, ps);

@@ -82,6 +82,42 @@ BRP_HD inline bool resamp_beyond_end(uint32_t m, float del_t, uint32_t n_unpadde
   return static_cast<float>(m) - del_t >= static_cast<float>(n_unpadded - 1);
 }
 
+// Number of resampled samples taken from the series (the rest is padding):
+// the reference scans down from N_u - 1 while the sample maps beyond the end
+// (demod_binary_resamp_cpu.c:94-99). m - del_t(m) rises monotonically
+// (|tau * Omega| << 1), so the crossing is bracketed by doubling steps and
+// bisection, and the reference's descending scan is replayed from 64 samples
+// above it: same result, ~30 instead of up to ~5000 LUT evaluations.
+inline uint32_t resamp_n_steps(const ResampParams& p, const float* sin_lut, const float* cos_lut) {
+  const uint32_t nu = p.nsamples_unpadded;
+  auto beyond = [&](uint32_t m) { return resamp_beyond_end(m, resamp_del_t(m, p, sin_lut, cos_lut), nu); };
+  uint32_t hi = nu - 1;
+  if (!beyond(hi)) return hi;
+  uint32_t lo = hi, span = 64;
+  for (;;) {
+    lo = hi > span ? hi - span : 0;
+    if (lo == 0 || !beyond(lo)) break;
+    hi = lo;
+    span *= 2;
+  }
+  while (hi - lo > 1) {
+    const uint32_t mid = lo + (hi - lo) / 2;
+    if (beyond(mid)) hi = mid;
+    else lo = mid;
+  }
+  uint32_t n = lo + 64 < nu - 1 ? lo + 64 : nu - 1;
+  while (n > 0 && beyond(n)) n--;
+  return n;
+}
+
+// The reference's plain descending scan (test oracle for resamp_n_steps).
+inline uint32_t resamp_n_steps_scan(const ResampParams& p, const float* sin_lut, const float* cos_lut) {
+  const uint32_t nu = p.nsamples_unpadded;
+  uint32_t n = nu - 1;
+  while (n > 0 && resamp_beyond_end(n, resamp_del_t(n, p, sin_lut, cos_lut), nu)) n--;
+  return n;
+}
+
 // Host-side derivation of the per-template parameters from one template-bank
 // line (demod_binary.c:1207-1238). Note the reference is compiled as C++, so
 // sin(float) resolves to the float overload.

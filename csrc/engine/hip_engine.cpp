@@ -283,9 +283,9 @@ struct HipEngine::Impl {
     const hipk::TwiddleTable tw = twt();
     switch (st) {
       case kPrologue:
-        e = hipMemcpyAsync(in.p, h_in.p, thr_bytes + sizeof(TemplateDev) * nb, hipMemcpyHostToDevice, stream);
-        if (e != hipSuccess) return e;
-        return hipk::launch_nsteps(tmpl.p, nb, stream, &cands.p[0].x);
+        // n_steps comes with the parameters (host bracketed search); pass 1
+        // zeroes the batch's candidate counter
+        return hipMemcpyAsync(in.p, h_in.p, thr_bytes + sizeof(TemplateDev) * nb, hipMemcpyHostToDevice, stream);
       case kPass1: {
         if (two_pass) {
           hipk::ColAArgs aa{};
@@ -297,6 +297,7 @@ struct HipEngine::Impl {
           aa.partials = partials.p;
           aa.tw = tw;
           aa.w768 = t_w768.p;
+          aa.reset = &cands.p[0].x;
           return hipk::launch_colA(aa, nb, stream);
         }
         hipk::Pass1Args a1{};
@@ -309,6 +310,7 @@ struct HipEngine::Impl {
         a1.n_unpadded = g.n_unpadded;
         a1.tmpl = tmpl.p;
         a1.partials = partials.p;
+        a1.reset = &cands.p[0].x;
         return hipk::launch_pass1(plan, hipk::P1_RESAMPLE, a1, nb, stream);
       }
       case kPass2: {
@@ -715,7 +717,7 @@ int HipEngine::process(const TemplateInput* t, int n, const float* thr, int thr_
       TemplateDev td{};
       td.p = make_resamp_params(g.nsamples, g.n_unpadded, g.fft_size, g.dt, g.step_inv, t[off + k].P,
                                 t[off + k].tau, t[off + k].Psi0);
-      td.n_steps = 0;
+      td.n_steps = resamp_n_steps(td.p, kSinLut, kCosLut);
       if (t[off + k].wu >= d.slots) return RADPUL_EVAL;
       td.wu = t[off + k].wu;
       td.mu0 = d.mu0s[td.wu];
@@ -798,11 +800,11 @@ int HipEngine::power_spectrum(const TemplateInput& t, std::vector<float>& ps_out
   TemplateDev td{};
   td.p = make_resamp_params(g.nsamples, g.n_unpadded, g.fft_size, g.dt, g.step_inv, t.P, t.tau, t.Psi0);
   td.mu0 = d.mu0s[0];
+  td.n_steps = resamp_n_steps(td.p, kSinLut, kCosLut);
   d.h_tmpl.p[0] = td;
   hipStream_t s = d.stream;
   BRP_HIP_CHECK(hipMemcpyAsync(d.tmpl.p, d.h_tmpl.p, sizeof(TemplateDev), hipMemcpyHostToDevice, s),
                 RADPUL_HIP_MEM_COPY_HOST_DEVICE);
-  BRP_HIP_CHECK(hipk::launch_nsteps(d.tmpl.p, 1, s), RADPUL_HIP_KERNEL_INVOKE);
   const hipk::TwiddleTable tw = d.twt();
   if (d.two_pass) {
     // the template pipeline's transform: pass A, pass B, transpose (all bins)
@@ -913,6 +915,7 @@ int HipEngine::benchmark_stages(const TemplateInput* t, int n, int reps, std::ve
   for (int k = 0; k < nb; ++k) {
     TemplateDev td{};
     td.p = make_resamp_params(g.nsamples, g.n_unpadded, g.fft_size, g.dt, g.step_inv, t[k].P, t[k].tau, t[k].Psi0);
+    td.n_steps = resamp_n_steps(td.p, kSinLut, kCosLut);
     td.mu0 = d.mu0s[0];
     d.h_tmpl.p[k] = td;
     for (int h = 0; h < kNumHarmonicLevels; ++h) d.h_thr.p[k * hipk::kHsThrStride + h] = d.g.chi2_thr[h];

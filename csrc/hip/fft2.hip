@@ -56,6 +56,7 @@ __global__ void __launch_bounds__(kThrA) colA_kernel(ColAArgs a) {
   const int c = threadIdx.x % kCols;
   const int j = threadIdx.x / kCols;
   const uint32_t ncol = col0 + c;  // n'
+  if (a.reset != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *a.reset = 0;
 
   for (int i = threadIdx.x; i < kLutSize; i += kThrA) {
     lut_s[i] = kSinLut[i];

@@ -24,6 +24,7 @@ struct ColAArgs {
   double* partials;            // [batch][R / 16] sums of (sample - mu0)
   TwiddleTable tw;             // W_4M^e
   const float2* w768;          // W_768^e, e < 768
+  uint32_t* reset;             // zeroed by workgroup (0, 0) when non-null (the batch's candidate counter)
 };
 
 // pass B: 8192-point row FFTs of row pairs + untangle + power spectrum (slab-major)

@@ -52,6 +52,7 @@ struct Pass1Args {
   uint32_t n_unpadded;
   const TemplateDev* tmpl;     // [batch]
   double* partials;            // [batch][wg1] sums of (sample - mu0)
+  uint32_t* reset;             // zeroed by workgroup (0, 0) when non-null (the batch's candidate counter)
   // P1_REAL
   const float* real_in;
   uint32_t n_real;

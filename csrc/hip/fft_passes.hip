@@ -47,6 +47,7 @@ __global__ void __launch_bounds__(kNcol * tpc_for<L>()) pass1_kernel(Pass1Args a
 
   int c, tj;
   Lay::coords(threadIdx.x, c, tj);
+  if (a.reset != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *a.reset = 0;
 
   double sum = 0.0;
   bool pruned = false;
@@ -169,6 +170,7 @@ __global__ void __launch_bounds__(kNcol * 16) pass1_pruned3_kernel(Pass1Args a) 
   const size_t M = static_cast<size_t>(L) * a.L2L3;
   const int c = threadIdx.x % kNcol;
   const int tj = threadIdx.x / kNcol;
+  if (a.reset != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *a.reset = 0;
 
   for (int i = threadIdx.x; i < kLutSize; i += NT) {
     lut_s[i] = kSinLut[i];

@@ -100,3 +100,25 @@ def test_cpu_rfft(brp, n):
     y = brp.irfft(X, n)
     # unnormalised c2r (FFTW semantics): n * x
     np.testing.assert_allclose(y, x * n, atol=1e-8 * n)
+
+
+@pytest.mark.parametrize("padding", [1.0, 3.0])
+def test_n_steps_search_equals_reference_scan(brp, padding):
+    """The bracketed n_steps search uploaded by the HIP engine equals the
+    reference's descending scan (demod_binary_resamp_cpu.c:94-99) for every
+    template of the benchmark bank and for extreme synthetic orbits."""
+    from conftest import BANK, WU
+
+    hdr, _, _ = brp.read_work_unit(str(WU))
+    geom = brp.derive_geometry(hdr, dict(f0=400.0, padding=padding, fA=0.08, window=1000))
+    P, tau, psi = brp.read_template_bank(str(BANK))
+    P, tau, psi = (np.asarray(v, dtype=np.float32) for v in (P, tau, psi))
+    fast = brp.n_steps(geom, P, tau, psi)
+    ref = brp.n_steps(geom, P, tau, psi, scan=True)
+    assert np.array_equal(fast, ref)
+    rng = np.random.default_rng(5)
+    n = 4000
+    Ps = rng.uniform(300.0, 5000.0, n).astype(np.float32)
+    taus = rng.uniform(0.0, 2.0, n).astype(np.float32)
+    psis = rng.uniform(0.0, 2 * np.pi, n).astype(np.float32)
+    assert np.array_equal(brp.n_steps(geom, Ps, taus, psis), brp.n_steps(geom, Ps, taus, psis, scan=True))
