@@ -149,9 +149,14 @@ template <int L, int NCOL, int TPC, bool ROWMAJOR>
 struct BlockLayout {
   static constexpr int kThreads = NCOL * TPC;
   static constexpr int kPitch = row_pitch<L>();
-  static constexpr int kLds = ROWMAJOR ? NCOL * kPitch : L * NCOL;  // float2 elements
+  // Row layout: slot c also gets a skew of 4 (c / 2) elements. Slot pairs
+  // (2i, 2i+1) keep the pitch == 16 (mod 32) spacing that the two-row stage
+  // accesses need, while the 8 slots a wave touches in the untangle (lanes
+  // walk slots, then 4 consecutive bins) start on 8 distinct 8-dword bank
+  // groups instead of 2 (measured: 25 % of pass 3's LDS cycles were conflicts).
+  static constexpr int kLds = ROWMAJOR ? NCOL * kPitch + 4 * (NCOL / 2) : L * NCOL;  // float2 elements
   __device__ __forceinline__ static int idx(int r, int c) {
-    return ROWMAJOR ? c * kPitch + r + (r >> 4) : r * NCOL + c;
+    return ROWMAJOR ? c * kPitch + 4 * (c >> 1) + r + (r >> 4) : r * NCOL + c;
   }
   __device__ __forceinline__ static void coords(int tid, int& c, int& tj) {
     if (ROWMAJOR) {
