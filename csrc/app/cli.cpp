@@ -13,6 +13,7 @@
 #include "../boinc/ipc.hpp"
 #include "../core/errors.hpp"
 #include "../core/log.hpp"
+#include "../engine/backend.hpp"
 #include "search.hpp"
 
 #ifndef BRP_GIT_ID
@@ -42,6 +43,7 @@ void print_usage(const char* prog) {
   std::printf(" --mi355x-gpus\t\tinteger\tGPUs (or CPU worker threads with --mi355x-cpu) driven by this process (default 1).\n");
   std::printf(" --mi355x-cpu\t\t\tboolean\tUse the CPU golden backend.\n");
   std::printf(" --mi355x-ps-fp16\t\tboolean\tStore the power spectrum as fp16 (needs -W).\n");
+  std::printf(" --mi355x-spin\t\t\tboolean\tBusy-wait for the GPU instead of sleeping (default: blocking sync).\n");
   std::printf("\n");
 }
 
@@ -51,6 +53,7 @@ bool is(const char* a, const char* s, const char* l) { return std::strcmp(a, s) 
 
 int search_main(int argc, char** argv) {
   SearchOptions opt;
+  bool spin = false;  // --mi355x-spin: busy-wait host synchronisation
   SearchControl ctl;
   int i = 1;
   auto need = [&](int k) -> const char* {
@@ -169,6 +172,10 @@ int search_main(int argc, char** argv) {
       i += 2;
     } else if (std::strcmp(a, "--mi355x-ps-fp16") == 0) {
       opt.ps_fp16 = true;
+      i++;
+    } else if (std::strcmp(a, "--mi355x-spin") == 0) {
+      spin = true;
+      i++;
     } else if (std::strcmp(a, "--mi355x-cpu") == 0) {
       opt.use_cpu = true;
       i++;
@@ -180,6 +187,9 @@ int search_main(int argc, char** argv) {
       return RADPUL_EMISC;
     }
   }
+  // a BOINC app shares the host: wait for the GPU by sleeping, as the
+  // reference's blocking-sync context does, unless --mi355x-spin
+  hip_set_blocking_sync(!spin);
   SearchResult res;
   int rc = run_search(opt, ctl, res);
   if (rc == 0 && res.templates_run > 0) {
@@ -214,6 +224,7 @@ int wrapper_main(int argc, char** argv) {
                                          {"mi355x-gpus", required_argument, 0, 1002},
                                          {"mi355x-cpu", no_argument, 0, 1003},
                                          {"mi355x-ps-fp16", no_argument, 0, 1004},
+                                         {"mi355x-spin", no_argument, 0, 1005},
                                          {0, 0, 0, 0}};
   optind = 1;
   auto file_arg = [&](const char* opt, const char* val) {
@@ -253,6 +264,7 @@ int wrapper_main(int argc, char** argv) {
       case 1002: fwd.push_back("--mi355x-gpus"); fwd.push_back(optarg); break;
       case 1003: fwd.push_back("--mi355x-cpu"); break;
       case 1004: fwd.push_back("--mi355x-ps-fp16"); break;
+      case 1005: fwd.push_back("--mi355x-spin"); break;
       default: boinc::finish(EINSTEINRADIO_EOPT);
     }
   }

@@ -53,5 +53,8 @@ std::unique_ptr<Backend> make_cpu_backend();
 // (N even and N/2 = L1*L2*L3 over the compiled lengths, fft_passes.hip).
 bool hip_backend_supports(const SearchGeometry& g);
 std::unique_ptr<Backend> make_hip_backend(int device, int batch, int* err);
+// Host waits on HIP work sleep (hipDeviceScheduleBlockingSync) instead of
+// spinning; set before the first backend is created (the BOINC app does).
+void hip_set_blocking_sync(bool on);
 
 }  // namespace brp

@@ -414,6 +414,38 @@ HipEngine::~HipEngine() {
   delete impl_;
 }
 
+namespace {
+bool g_blocking_sync = false;
+
+// Standalone device choice when neither -D, BOINC's gpu_device_num nor
+// BRP_DEVICE names one: the device with the highest CU count x clock
+// (reference findBestFreeDevice, cuda/app/cuda_utilities.c:96-237, by GFLOPS;
+// device properties only, no context is created on the other GPUs).
+int best_device(int ndev) {
+  int best = 0;
+  double best_score = -1.0;
+  for (int d = 0; d < ndev; ++d) {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, d) != hipSuccess) continue;
+    const double score = static_cast<double>(prop.multiProcessorCount) * prop.clockRate;
+    if (score > best_score) {
+      best_score = score;
+      best = d;
+    }
+  }
+  return best;
+}
+
+void log_mem_status(int device, const char* when) {
+  size_t free_b = 0, total_b = 0;
+  if (hipMemGetInfo(&free_b, &total_b) == hipSuccess)
+    log_message(LOG_DEBUG, true, "HIP device #%d global memory %s: %.1f MB free of %.1f MB\n", device, when,
+                free_b / 1e6, total_b / 1e6);
+}
+}  // namespace
+
+void hip_set_blocking_sync(bool on) { g_blocking_sync = on; }
+
 int HipEngine::init(int device, int batch) {
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
@@ -422,13 +454,21 @@ int HipEngine::init(int device, int batch) {
   }
   if (device < 0) {
     const char* env = std::getenv("BRP_DEVICE");
-    device = env ? std::atoi(env) : 0;
+    device = env ? std::atoi(env) : best_device(ndev);
   }
   if (device >= ndev) {
     log_message(LOG_ERROR, true, "Requested device %d but only %d present.\n", device, ndev);
     return RADPUL_HIP_DEVICE_SET;
   }
   BRP_HIP_CHECK(hipSetDevice(device), RADPUL_HIP_DEVICE_SET);
+  if (g_blocking_sync) {
+    // host waits sleep instead of spinning (reference CU_CTX_BLOCKING_SYNC with
+    // fallback to automatic scheduling, cuda/app/demod_binary_cuda.cu:126-137)
+    if (hipSetDeviceFlags(hipDeviceScheduleBlockingSync) != hipSuccess) {
+      (void)hipGetLastError();
+      log_message(LOG_WARN, true, "Blocking synchronisation unavailable (context exists): automatic scheduling.\n");
+    }
+  }
   impl_->device = device;
   impl_->batch = batch > 0 ? batch : 4;
   BRP_HIP_CHECK(hipStreamCreateWithFlags(&impl_->stream, hipStreamNonBlocking), RADPUL_HIP_DEVICE_SET);
@@ -527,6 +567,7 @@ int HipEngine::setup(const SearchGeometry& g, const std::vector<float>& series, 
   if ((rc = d.build_tables())) return rc;
   BRP_HIP_CHECK(hipMemcpy(d.series.p, series.data(), g.n_unpadded * sizeof(float), hipMemcpyHostToDevice),
                 RADPUL_HIP_MEM_COPY_HOST_DEVICE);
+  log_mem_status(d.device, "after setup");
   d.ready = true;
   return 0;
 }

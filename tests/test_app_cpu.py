@@ -179,3 +179,19 @@ def test_unsupported_fft_length_falls_back_to_cpu(brp, case, tmp_path):
     assert out.templates_run == 3
     M = out.geometry["nsamples"] // 2
     assert brp.fft_plan(M) is None
+
+
+def test_app_mi355x_flags_parse(app, case, tmp_path):
+    """The MI355X option namespace parses without disturbing the BOINC options
+    (a flag that did not advance the parser used to hang the app); results
+    with --mi355x-spin / --mi355x-ps-fp16 on the CPU backend equal the plain run."""
+    (tmp_path / "a").mkdir()
+    (tmp_path / "b").mkdir()
+    r0 = _run_app(app, _app_args(case, tmp_path / "a"), tmp_path)
+    assert r0.returncode == 0, r0.stderr[-2000:]
+    r1 = _run_app(app, _app_args(case, tmp_path / "b", ["--mi355x-spin", "--mi355x-batch", "3"]), tmp_path)
+    assert r1.returncode == 0, r1.stderr[-2000:]
+    assert (tmp_path / "a" / "res.cand").read_text() == (tmp_path / "b" / "res.cand").read_text()
+    (tmp_path / "c").mkdir()
+    r2 = _run_app(app, _app_args(case, tmp_path / "c", ["--mi355x-ps-fp16", "-h"]), tmp_path)
+    assert "--mi355x-spin" in r2.stdout + r2.stderr
