@@ -20,7 +20,7 @@ for s, e, _ in iv:
 busy += cur_e - cur_s
 per = defaultdict(int)
 for s, e, n in iv:
-    per[n.split("(")[0][-60:]] += e - s
+    per[n.replace("(anonymous namespace)::", "").split("(")[0][-60:]] += e - s
 span = t1 - t0
 print(f"span {span/1e6:.2f} ms  busy {busy/1e6:.2f} ms ({100*busy/span:.1f} %)  dispatches {len(iv)}")
 for n, v in sorted(per.items(), key=lambda x: -x[1])[:10]:
