@@ -77,16 +77,31 @@ def _needs(obj: Path, src: Path, hdr_mtime: float, force: bool) -> bool:
     return obj.stat().st_mtime < max(src.stat().st_mtime, hdr_mtime)
 
 
-def _compile(src_rel: str, force: bool, hdr_mtime: float) -> tuple[str, Path]:
+# Host-code sanitizers: the app is also built with ASan +
+# UBSan on every host translation unit (device code is not instrumented: GPU
+# sanitizers are not available on the MI355X pool). On hipcc lines each
+# -fsanitize= follows -Xarch_host so only the host compilation sees it.
+SAN = ["address", "undefined"]
+OBJ_SAN = ROOT / "build" / "obj_asan"
+
+
+def asan_app_path() -> Path:
+    return BIN / "einsteinbinary_mi355x_asan"
+
+
+def _compile(src_rel: str, force: bool, hdr_mtime: float, sanitize: bool = False) -> tuple[str, Path]:
     src = CSRC / src_rel
-    obj = OBJ / (src_rel.replace("/", "__") + ".o")
+    obj = (OBJ_SAN if sanitize else OBJ) / (src_rel.replace("/", "__") + ".o")
     if not _needs(obj, src, hdr_mtime, force):
         return "cached", obj
     obj.parent.mkdir(parents=True, exist_ok=True)
+    san_host = [f for s in SAN for f in ("-Xarch_host", f"-fsanitize={s}")] if sanitize else []
+    san_cxx = [f"-fsanitize={s}" for s in SAN] + ["-fno-omit-frame-pointer", "-g"] if sanitize else []
     if src.suffix == ".hip":
-        cmd = [HIPCC, f"--offload-arch={ARCH}", *_common_flags(), "-munsafe-fp-atomics", "-c", str(src), "-o", str(obj)]
+        cmd = [HIPCC, f"--offload-arch={ARCH}", *_common_flags(), "-munsafe-fp-atomics", *san_host,
+               *(["-Xarch_host", "-fno-omit-frame-pointer"] if sanitize else []), "-c", str(src), "-o", str(obj)]
     else:
-        flags = _common_flags()
+        flags = _common_flags() + san_cxx
         if src_rel.startswith("bindings/"):
             import pybind11
             flags += [f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}",
@@ -98,11 +113,13 @@ def _compile(src_rel: str, force: bool, hdr_mtime: float) -> tuple[str, Path]:
     return "built", obj
 
 
-def _link(objs: list[Path], out: Path, shared: bool) -> None:
+def _link(objs: list[Path], out: Path, shared: bool, sanitize: bool = False) -> None:
     out.parent.mkdir(parents=True, exist_ok=True)
     tmp = out.with_name(out.name + ".tmp")
     cmd = [HIPCC, f"--offload-arch={ARCH}", *[str(o) for o in objs], "-o", str(tmp),
            f"-L{ROCM / 'lib'}", "-lamdhip64", "-lz", "-lpthread"]
+    if sanitize:
+        cmd += [f"-fsanitize={s}" for s in SAN]
     if shared:
         cmd.insert(1, "-shared")
     else:
@@ -141,12 +158,37 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = True) ->
     return {"extension": str(ext), "app": str(app)}
 
 
+def build_asan(force: bool = False, jobs: int | None = None, verbose: bool = True) -> Path:
+    """ASan + UBSan build of the application binary (host code instrumented)."""
+    jobs = jobs or min(16, os.cpu_count() or 4)
+    hdr = _headers_mtime()
+    srcs = HOST_SRCS + DEVICE_SRCS + [APP_MAIN]
+    results = {}
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        futs = {ex.submit(_compile, s, force, hdr, True): s for s in srcs}
+        for f in cf.as_completed(futs):
+            status, obj = f.result()
+            results[futs[f]] = obj
+            if verbose and status == "built":
+                print(f"[build asan] {futs[f]}", flush=True)
+    objs = [results[s] for s in srcs]
+    app = asan_app_path()
+    if force or not app.exists() or app.stat().st_mtime < max(o.stat().st_mtime for o in objs):
+        _link(objs, app, shared=False, sanitize=True)
+        if verbose:
+            print(f"[build asan] linked {app.relative_to(ROOT)}", flush=True)
+    return app
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", "--jobs", type=int, default=None)
+    ap.add_argument("--asan", action="store_true", help="also build bin/einsteinbinary_mi355x_asan (ASan + UBSan)")
     a = ap.parse_args(argv)
     out = build(force=a.force, jobs=a.jobs)
+    if a.asan:
+        out["asan_app"] = str(build_asan(force=a.force, jobs=a.jobs))
     print(out)
     return 0
 
