@@ -39,11 +39,12 @@ void print_usage(const char* prog) {
   std::printf(" -B, --box\t\t\tint\tWindow width for the running median in frequeny bins.\n");
   std::printf(" -D, --device\t\tinteger\tThe GPU device ID to be used.\n");
   std::printf(" -z, --debug\t\t\tboolean\tRun program in debug mode.\n");
-  std::printf(" --mi355x-batch\t\tinteger\tTemplates per device batch (default 4).\n");
+  std::printf(" --mi355x-batch\t\tinteger\tTemplates per device batch (default 1).\n");
   std::printf(" --mi355x-gpus\t\tinteger\tGPUs (or CPU worker threads with --mi355x-cpu) driven by this process (default 1).\n");
   std::printf(" --mi355x-cpu\t\t\tboolean\tUse the CPU golden backend.\n");
   std::printf(" --mi355x-ps-fp16\t\tboolean\tStore the power spectrum as fp16 (needs -W).\n");
   std::printf(" --mi355x-spin\t\t\tboolean\tBusy-wait for the GPU instead of sleeping (default: blocking sync).\n");
+  std::printf(" --mi355x-pipelines\t\tinteger\tIndependent pipelines per GPU (default 3, one template each).\n");
   std::printf("\n");
 }
 
@@ -55,6 +56,10 @@ int search_main(int argc, char** argv) {
   SearchOptions opt;
   bool spin = false;  // --mi355x-spin: busy-wait host synchronisation
   SearchControl ctl;
+  // measured best on one MI355X: 3 pipelines of one template each (the FFT
+  // intermediates of every pipeline stay in the Infinity Cache)
+  ctl.pipelines = 3;
+  opt.batch = 1;
   int i = 1;
   auto need = [&](int k) -> const char* {
     if (k + 1 >= argc) return nullptr;
@@ -170,6 +175,10 @@ int search_main(int argc, char** argv) {
       if (!v) return RADPUL_EVAL;
       ctl.gpus = std::max(1, std::atoi(v));
       i += 2;
+    } else if (std::strcmp(a, "--mi355x-pipelines") == 0) {
+      if (!v) return RADPUL_EVAL;
+      ctl.pipelines = std::max(1, std::atoi(v));
+      i += 2;
     } else if (std::strcmp(a, "--mi355x-ps-fp16") == 0) {
       opt.ps_fp16 = true;
       i++;
@@ -225,6 +234,7 @@ int wrapper_main(int argc, char** argv) {
                                          {"mi355x-cpu", no_argument, 0, 1003},
                                          {"mi355x-ps-fp16", no_argument, 0, 1004},
                                          {"mi355x-spin", no_argument, 0, 1005},
+                                         {"mi355x-pipelines", required_argument, 0, 1006},
                                          {0, 0, 0, 0}};
   optind = 1;
   auto file_arg = [&](const char* opt, const char* val) {
@@ -265,6 +275,7 @@ int wrapper_main(int argc, char** argv) {
       case 1003: fwd.push_back("--mi355x-cpu"); break;
       case 1004: fwd.push_back("--mi355x-ps-fp16"); break;
       case 1005: fwd.push_back("--mi355x-spin"); break;
+      case 1006: fwd.push_back("--mi355x-pipelines"); fwd.push_back(optarg); break;
       default: boinc::finish(EINSTEINRADIO_EOPT);
     }
   }

@@ -209,14 +209,18 @@ int SearchSession::open(const SearchOptions& opt, const SearchControl& ctl) {
     d.opt.use_cpu = true;
     ngpu = nt;
   }
+  // HIP: ctl.pipelines backends per device, consecutive backends on one device
+  const int per_dev = d.opt.use_cpu ? 1 : std::max(1, ctl.pipelines);
+  const int nback = ngpu * per_dev;
   boinc::begin_critical_section();
-  for (int k = 0; k < ngpu; ++k) {
+  for (int kb = 0; kb < nback; ++kb) {
+    const int k = kb / per_dev;  // device index
     std::unique_ptr<Backend> b;
     if (d.opt.use_cpu) {
       b = make_cpu_backend();
     } else {
       int dev = opt.device;
-      if (!ctl.devices.empty()) dev = ctl.devices[k % ctl.devices.size()];
+      if (!ctl.devices.empty()) dev = ctl.devices[kb % ctl.devices.size()];
       else if (ngpu > 1) dev = k;
       else if (dev < 0 && boinc::init_data().gpu_device_num >= 0) dev = boinc::init_data().gpu_device_num;
       int err = 0;
@@ -238,6 +242,9 @@ int SearchSession::prepare() {
   SearchOptions opt_nw = d.opt;
   opt_nw.white = false;
   opt_nw.prewhitened = d.opt.white;
+  // the other backends take the whitened series (~11 ms each on MI355X;
+  // concurrent setups from several host threads measured no faster: the HIP
+  // runtime serialises the allocations and uploads)
   for (size_t k = 1; k < d.backends.size(); ++k) {
     std::vector<float> s = d.series;
     rc = d.backends[k]->setup(d.g, opt_nw, s, d.zaps);

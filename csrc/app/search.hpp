@@ -31,6 +31,7 @@ struct SearchControl {
   bool write_output = true;       // result file + final checkpoint
   bool use_checkpoint = true;
   int gpus = 1;                   // devices driven by this process (in-order merge)
+  int pipelines = 1;              // independent pipelines (stream + buffers) per device
   std::vector<int> devices;       // explicit device ids (optional)
   // called after every template applied (progress hooks / fault injection)
   std::function<void(uint32_t done, uint32_t total)> on_template;

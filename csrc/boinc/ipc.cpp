@@ -75,7 +75,7 @@ void update_shmem(const SearchInfo& info) {
   const std::string doc = render_xml(info);
   std::memset(g_shmem, 0, kShmemSize);
   if (!doc.empty() && doc.size() < static_cast<size_t>(kShmemSize)) {
-    std::snprintf(g_shmem, doc.size(), "%s", doc.c_str());
+    std::memcpy(g_shmem, doc.data(), doc.size());  // NUL-terminated by the memset
   } else {
     std::fprintf(stderr, "Error writing shared memory data (size limit exceeded)!\n");
   }
