@@ -157,7 +157,8 @@ struct HipEngine::Impl {
   bool ready = false;
   uint32_t num_cus = 256;
   bool ps_fp16 = false;         // config 5: fp16 power spectrum between pass 3 and the harmonic sum
-  bool hs_gather = std::getenv("BRP_HS_STAGED") == nullptr;  // LDS-staged segments only on request (measured slower)
+  // harmonic-sum variant: harmonics 1..n staged in LDS, the rest gathered (BRP_HS_STAGE)
+  int hs_stage = std::getenv("BRP_HS_STAGE") ? std::atoi(std::getenv("BRP_HS_STAGE")) : 0;
   uint32_t persist_per_cu = 4;  // persistent FFT passes: workgroups per CU (BRP_PERSIST, 0 = off)
   uint32_t ps_stride = 0;
   uint32_t i_start = 0;
@@ -389,7 +390,7 @@ struct HipEngine::Impl {
         ah.thr = thr.p;
         ah.list = cands.p;
         ah.cap = cap;
-        ah.gather = hs_gather;
+        ah.staged_harmonics = hs_stage;
         return hipk::launch_harmonic_sum(ah, nb, stream);
       }
       case kEpilogue:

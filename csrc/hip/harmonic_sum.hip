@@ -54,39 +54,43 @@ __device__ __forceinline__ void emit(uint32_t* counter, uint2* list, uint32_t ca
 // l starts at the 4-aligned bin lo4(l) and occupies kStageCap(l) floats.
 __host__ __device__ constexpr int stage_cap(int l) { return ((l * (kSpan - 1) / 16 + 5 + 3) / 4) * 4; }
 __host__ __device__ constexpr int stage_off(int l) { return l <= 1 ? 0 : stage_off(l - 1) + stage_cap(l - 1); }
-constexpr int kStageFloats = stage_off(17);
 // per harmonic l: ceil(chunks / threads) load iterations
 __host__ __device__ constexpr int stage_iters(int l) { return (stage_cap(l) / 4 + kThreads - 1) / kThreads; }
 __host__ __device__ constexpr int stage_iters_before(int l) { return l <= 1 ? 0 : stage_iters_before(l - 1) + stage_iters(l - 1); }
-__host__ __device__ constexpr int stage_iters_total() { return stage_iters_before(17); }
+// LDS floats of the kernel staging harmonics 1..smax (S_1..S_4 alias the area)
+__host__ __device__ constexpr int stage_lds_floats(int smax) {
+  return stage_off(smax + 1) > 4 * kSpanPad ? stage_off(smax + 1) : 4 * kSpanPad;
+}
 
 // f(integral_constant<l>, integral_constant<it>, flat iteration base) for
-// l = 1..16 and it < stage_iters(l), fully unrolled
-template <int L, int IT, typename F>
+// l = 1..LMAX and it < stage_iters(l), fully unrolled
+template <int LMAX, int L, int IT, typename F>
 __device__ __forceinline__ void stage_for_each_impl(F&& f) {
-  if constexpr (L <= 16) {
+  if constexpr (L <= LMAX) {
     if constexpr (IT < stage_iters(L)) {
       f(std::integral_constant<int, L>{}, std::integral_constant<int, IT>{}, stage_iters_before(L));
-      stage_for_each_impl<L, IT + 1>(f);
+      stage_for_each_impl<LMAX, L, IT + 1>(f);
     } else {
-      stage_for_each_impl<L + 1, 0>(f);
+      stage_for_each_impl<LMAX, L + 1, 0>(f);
     }
   }
 }
-template <typename F>
+template <int LMAX, typename F>
 __device__ __forceinline__ void stage_for_each(F&& f) {
-  stage_for_each_impl<1, 0>(f);
+  stage_for_each_impl<LMAX, 1, 0>(f);
 }
-static_assert(kStageFloats >= 4 * kSpanPad, "S_1..S_4 alias the staging area");
 
 // T = float (exact path) or _Float16 (config 5 spectrum); every element is
-// widened to float before the reference-order float sums. STAGED: harmonic
-// segments staged in LDS (default) or gathered per i from global memory.
-template <typename T, bool STAGED>
+// widened to float before the reference-order float sums. Harmonics 1..SMAX
+// are staged in LDS (their runs are short, l/16 bins per i, and shared by
+// many lanes of a gather), harmonics SMAX+1..16 are gathered per i from
+// global memory: SMAX = 0 gathers all, 16 stages all.
+template <typename T, int SMAX>
 __global__ void __launch_bounds__(kThreads) harmonic_sum_kernel(HSArgs a) {
 #pragma clang fp contract(off)
+  constexpr bool STAGED = SMAX > 0;
   // staged segments, then (after a barrier) S_1..S_4 over the tile + halo
-  __shared__ __attribute__((aligned(16))) float lds[STAGED ? kStageFloats : 4 * kSpanPad];
+  __shared__ __attribute__((aligned(16))) float lds[stage_lds_floats(SMAX)];
   float (*sv)[kSpanPad] = reinterpret_cast<float (*)[kSpanPad]>(lds);
   const int b = blockIdx.y;
   const T* P = reinterpret_cast<const T*>(sizeof(T) == 4 ? static_cast<const void*>(a.ps)
@@ -96,14 +100,14 @@ __global__ void __launch_bounds__(kThreads) harmonic_sum_kernel(HSArgs a) {
   const float ninf = -__builtin_inff();
   auto lo4 = [&](uint32_t l) { return ((l * i0 + 8u) >> 4) & ~3u; };
 
-  if (STAGED) {
+  if constexpr (STAGED) {
     // harmonic by harmonic (compile-time l: the run's origin is a scalar and
     // no per-lane selection is needed); every load is issued before the first
     // LDS write. Chunks past the spectrum's stride read as zero (only i >= hhi
     // would use them).
-    constexpr int kIters = stage_iters_total();
+    constexpr int kIters = stage_iters_before(SMAX + 1);
     float4 v[kIters];
-    stage_for_each([&](auto l_tag, auto it_tag, int it_base) {
+    stage_for_each<SMAX>([&](auto l_tag, auto it_tag, int it_base) {
       constexpr int l = decltype(l_tag)::value;
       constexpr int it = decltype(it_tag)::value;
       constexpr int nch = stage_cap(l) / 4;
@@ -123,7 +127,7 @@ __global__ void __launch_bounds__(kThreads) harmonic_sum_kernel(HSArgs a) {
         }
       }
     });
-    stage_for_each([&](auto l_tag, auto it_tag, int it_base) {
+    stage_for_each<SMAX>([&](auto l_tag, auto it_tag, int it_base) {
       constexpr int l = decltype(l_tag)::value;
       constexpr int it = decltype(it_tag)::value;
       const int ch = static_cast<int>(threadIdx.x) + it * kThreads;
@@ -133,7 +137,7 @@ __global__ void __launch_bounds__(kThreads) harmonic_sum_kernel(HSArgs a) {
   }
   auto ld = [&](uint32_t l, uint32_t i) -> float {
     const uint32_t bin = (l * i + 8u) >> 4;
-    if (STAGED) return lds[stage_off(static_cast<int>(l)) + static_cast<int>(bin - lo4(l))];
+    if (static_cast<int>(l) <= SMAX) return lds[stage_off(static_cast<int>(l)) + static_cast<int>(bin - lo4(l))];
     return static_cast<float>(P[bin]);
   };
 
@@ -158,7 +162,7 @@ __global__ void __launch_bounds__(kThreads) harmonic_sum_kernel(HSArgs a) {
       s4[it] = sum;
     }
   }
-  if (STAGED) __syncthreads();  // staging area becomes sv
+  if constexpr (STAGED) __syncthreads();  // staging area becomes sv
 #pragma unroll
   for (int it = 0; it < kIt; ++it) {
     const int t = threadIdx.x + it * kThreads;
@@ -224,13 +228,17 @@ hipError_t launch_harmonic_sum(const HSArgs& a, int batch, hipStream_t s) {
   const uint32_t tiles = hs_num_tiles(a.i_start, a.hhi);
   if (tiles == 0) return hipSuccess;
   const dim3 grid(tiles, batch);
-  if (a.gather) {
-    if (a.ps16 != nullptr) hipLaunchKernelGGL((harmonic_sum_kernel<_Float16, false>), grid, dim3(kThreads), 0, s, a);
-    else hipLaunchKernelGGL((harmonic_sum_kernel<float, false>), grid, dim3(kThreads), 0, s, a);
-  } else {
-    if (a.ps16 != nullptr) hipLaunchKernelGGL((harmonic_sum_kernel<_Float16, true>), grid, dim3(kThreads), 0, s, a);
-    else hipLaunchKernelGGL((harmonic_sum_kernel<float, true>), grid, dim3(kThreads), 0, s, a);
+#define BRP_HS_LAUNCH(SM)                                                                                   \
+  if (a.ps16 != nullptr) hipLaunchKernelGGL((harmonic_sum_kernel<_Float16, SM>), grid, dim3(kThreads), 0, s, a); \
+  else hipLaunchKernelGGL((harmonic_sum_kernel<float, SM>), grid, dim3(kThreads), 0, s, a);
+  switch (a.staged_harmonics) {
+    case 0: BRP_HS_LAUNCH(0) break;
+    case 4: BRP_HS_LAUNCH(4) break;
+    case 8: BRP_HS_LAUNCH(8) break;
+    case 16: BRP_HS_LAUNCH(16) break;
+    default: return hipErrorInvalidValue;
   }
+#undef BRP_HS_LAUNCH
   return hipGetLastError();
 }
 

@@ -21,7 +21,7 @@ struct HSArgs {
   // exceed cap), list[1 + q] = (hs_pack(template, level, bin), power bits)
   uint2* list;
   uint32_t cap;
-  bool gather;            // per-i global gathers instead of LDS-staged segments (A/B testing)
+  int staged_harmonics;   // harmonics 1..n staged in LDS (0, 4, 8 or 16), the rest gathered per i
 };
 
 constexpr uint32_t kHsThrStride = 8;  // floats per template in the threshold array (5 used)
