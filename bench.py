@@ -52,6 +52,9 @@ def parse():
                     help="work units resident per GPU (config 4): the reference WU + synthetic WUs of its shape")
     ap.add_argument("--synthetic", action="store_true", help="synthetic WU/bank of the benchmark shape")
     ap.add_argument("--write-output", default="", help="rank 0 writes the result file of the last step here")
+    ap.add_argument("--cpu", action="store_true",
+                    help="rehearsal of the multi-rank path without GPUs: gloo collectives, CPU golden backend, "
+                         "small synthetic WU (not a benchmark; used by tests/test_bench_cpu.py)")
     return ap.parse_args()
 
 
@@ -122,7 +125,8 @@ def main() -> int:
     from boinc_app_eah_brp_amd import native
     from boinc_app_eah_brp_amd.parallel import ShardedSearch, barrier, init_distributed, max_over_ranks
 
-    ctx = init_distributed()
+    ctx = init_distributed("gloo" if args.cpu else None)
+    use_gpu = torch.cuda.is_available() and not args.cpu
     world = ctx.world
     if world != args.gpus and ctx.rank == 0:
         print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}", file=sys.stderr)
@@ -130,11 +134,21 @@ def main() -> int:
     brp.set_log_level(2)
     wu, bank, zap = WU, BANK, ZAP
     data_desc = "real: reference test WU p2030...b2s0g0.00000_1099.bin4 (2^22 4-bit samples) + stochastic_full.bank"
-    if args.synthetic or not WU.exists():
+    window = 1000
+    if args.cpu:
+        from boinc_app_eah_brp_amd.utils import synth
+
+        case = synth.synthetic_case(Path(os.environ.get("TMPDIR", "/tmp")) / f"brp_bench_cpu_{ctx.rank}", n=1 << 15,
+                                    n_templates=24,
+                                    inj=synth.Injection(f0=211.0, P_orb=900.0, tau=0.03, psi0=0.7, amplitude=3.0))
+        wu, bank, zap = Path(case["wu"]), Path(case["bank"]), Path(case["zap"])
+        window = 100
+        data_desc = "synthetic CPU rehearsal of the multi-rank path (2^15 samples, 25 templates; not a benchmark)"
+    elif args.synthetic or not WU.exists():
         wu, bank, zap = synthetic_inputs(Path(os.environ.get("TMPDIR", "/tmp")) / f"brp_bench_{ctx.rank}")
         data_desc = "synthetic: 2^22-sample 4-bit WU with an injected binary pulsar + random 6662-template bank"
     opts = dict(inputfile=str(wu), templatebank=str(bank), zaplistfile=str(zap), f0=400.0, padding=3.0, fA=0.08,
-                window=1000, white=True, batch=args.batch, outputfile=args.write_output, ps_fp16=args.ps_fp16)
+                window=window, white=True, batch=args.batch, outputfile=args.write_output, ps_fp16=args.ps_fp16)
     n_wus = max(1, args.wus)
     if n_wus > 1:
         from boinc_app_eah_brp_amd.models import MultiWUSearch, SearchConfig
@@ -146,12 +160,12 @@ def main() -> int:
         search = MultiWUSearch([str(wu)] + extra, cfg, pipelines=args.streams, ctx=ctx)
         data_desc += f" + {n_wus - 1} synthetic WUs of the same shape (noise + injected binary pulsars)"
     else:
-        search = ShardedSearch(opts, ctx, streams=args.streams)
+        search = ShardedSearch(opts, ctx, streams=1 if args.cpu else args.streams, use_cpu=args.cpu)
     limit = args.templates if args.templates > 0 else search.total
 
     def first_table(t):
         return t[0] if isinstance(t, list) else t
-    if torch.cuda.is_available():
+    if use_gpu:
         torch.cuda.synchronize()
 
     table = None
@@ -159,14 +173,14 @@ def main() -> int:
         table = search.step(limit)
     first = bytes(first_table(table).to_bytes()) if table is not None else None
     barrier(ctx)
-    if torch.cuda.is_available():
+    if use_gpu:
         torch.cuda.synchronize()
     search.timings.clear()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         table = search.step(limit)
     barrier(ctx)
-    if torch.cuda.is_available():
+    if use_gpu:
         torch.cuda.synchronize()
     elapsed = max_over_ranks(time.perf_counter() - t0, ctx)
 
@@ -180,7 +194,7 @@ def main() -> int:
         total = limit * args.steps * n_wus
         value = total / elapsed
         n_cands = sum(1 for e in table.entries() if e[5] > 0)
-        rec = recall_vs_golden(table, geom) if limit == search.total else None
+        rec = recall_vs_golden(table, geom) if limit == search.total and not args.cpu else None
         out = {
             "metric": METRIC,
             "value": round(value, 2),

@@ -1,0 +1,42 @@
+"""The driver-facing bench.py contract on CPU: launched by torch.distributed.run
+with 2 and 4 ranks (gloo, CPU golden backend, small synthetic WU via --cpu),
+rank 0 prints exactly one JSON line with the whole-job value, and the sharded,
+all-gathered result file equals the single-rank one byte for byte."""
+import json
+import os
+import socket
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _bench(nproc, tmp, out):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", str(nproc),
+           "--steps", "1", "--warmup", "1", "--cpu", "--batch", "3", "--write-output", str(out)]
+    env = dict(os.environ, TMPDIR=str(tmp), OMP_NUM_THREADS="1", BRP_NO_RESULT_HEADER="1")
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("nproc", [2, 4])
+def test_bench_multirank_cpu_rehearsal(nproc, tmp_path):
+    one = _bench(1, tmp_path / "w1", tmp_path / "one.cand")
+    many = _bench(nproc, tmp_path / f"w{nproc}", tmp_path / "many.cand")
+    assert one["n_gpus"] == 1 and many["n_gpus"] == nproc
+    assert many["value"] > 0 and many["config"]["parallelism"].startswith(f"dp{nproc}")
+    assert many["table_identical_to_warmup"] is True
+    assert (tmp_path / "one.cand").read_text() == (tmp_path / "many.cand").read_text()
