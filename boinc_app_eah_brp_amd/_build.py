@@ -30,7 +30,7 @@ ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0]
 
 HOST_SRCS = [
     "core/log.cpp", "core/io.cpp", "core/stats.cpp", "core/gsl_compat.cpp", "core/rngmed.cpp",
-    "core/search_core.cpp", "core/cpu_fft.cpp", "core/cpu_backend.cpp",
+    "core/search_core.cpp", "core/cpu_fft.cpp", "core/cpu_backend.cpp", "core/wisdom.cpp",
     "boinc/boinc_shim.cpp", "boinc/ipc.cpp",
     "engine/cpu_engine.cpp", "engine/hip_engine.cpp",
     "app/search.cpp", "app/multi.cpp", "app/cli.cpp",
@@ -117,7 +117,7 @@ def _link(objs: list[Path], out: Path, shared: bool, sanitize: bool = False) -> 
     out.parent.mkdir(parents=True, exist_ok=True)
     tmp = out.with_name(out.name + ".tmp")
     cmd = [HIPCC, f"--offload-arch={ARCH}", *[str(o) for o in objs], "-o", str(tmp),
-           f"-L{ROCM / 'lib'}", "-lamdhip64", "-lz", "-lpthread"]
+           f"-L{ROCM / 'lib'}", "-lamdhip64", "-lz", "-lpthread", "-ldl"]
     if sanitize:
         cmd += [f"-fsanitize={s}" for s in SAN]
     if shared:

@@ -21,6 +21,7 @@
 #include "../core/rngmed.hpp"
 #include "../core/search_core.hpp"
 #include "../core/stats.hpp"
+#include "../core/wisdom.hpp"
 #include "../engine/hip_engine.hpp"
 
 namespace py = pybind11;
@@ -345,6 +346,18 @@ PYBIND11_MODULE(_brp, m) {
     float mean = 0;
     cpu_resample(series.data(), p, out, &n_steps, &mean);
     return py::make_tuple(py::array_t<float>(out.size(), out.data()), n_steps, mean);
+  });
+  m.def("wisdom_path", &wisdom_path);
+  m.def("load_wisdom", [](const std::string& path, const std::string& arch, uint32_t M) {
+    const PlanWisdom w = load_wisdom(path, arch, M);
+    py::dict d;
+    d["found"] = w.found;
+    d["persist_per_cu"] = w.persist_per_cu;
+    d["fft_passes"] = w.fft_passes;
+    d["hs_stage"] = w.hs_stage;
+    d["batch"] = w.batch;
+    d["pipelines"] = w.pipelines;
+    return d;
   });
   // n_steps of many templates: bracketed search (what the HIP engine uploads)
   // and the reference's descending scan

@@ -22,6 +22,7 @@
 #include "../core/cpu_backend.hpp"
 #include "../core/log.hpp"
 #include "../core/rngmed.hpp"
+#include "../core/wisdom.hpp"
 #include "../hip/fft2_kernels.hpp"
 #include "../hip/fft_kernels.hpp"
 #include "../hip/hs_kernels.hpp"
@@ -156,9 +157,10 @@ struct HipEngine::Impl {
   FFTPlan3 plan;
   bool ready = false;
   uint32_t num_cus = 256;
+  std::string arch;             // gcnArchName (plan-wisdom lookup)
   bool ps_fp16 = false;         // config 5: fp16 power spectrum between pass 3 and the harmonic sum
   // harmonic-sum variant: harmonics 1..n staged in LDS, the rest gathered (BRP_HS_STAGE)
-  int hs_stage = std::getenv("BRP_HS_STAGE") ? std::atoi(std::getenv("BRP_HS_STAGE")) : 0;
+  int hs_stage = 0;
   uint32_t persist_per_cu = 4;  // persistent FFT passes: workgroups per CU (BRP_PERSIST, 0 = off)
   uint32_t ps_stride = 0;
   uint32_t i_start = 0;
@@ -480,6 +482,7 @@ int HipEngine::init(int device, int batch) {
   log_message(LOG_INFO, true, "Using HIP device #%d: %s (%s, %d CUs, %.1f GB)\n", device, prop.name,
               prop.gcnArchName, prop.multiProcessorCount, prop.totalGlobalMem / 1e9);
   impl_->num_cus = static_cast<uint32_t>(prop.multiProcessorCount);
+  impl_->arch = prop.gcnArchName;
   return 0;
 }
 
@@ -515,12 +518,20 @@ int HipEngine::setup(const SearchGeometry& g, const std::vector<float>& series, 
                 g.nsamples);
     return RADPUL_HIP_FFT_PLAN;
   }
+  // measured settings for this (arch, M) from the plan wisdom; environment wins
+  const PlanWisdom wis = load_wisdom(wisdom_path(), d.arch, d.plan.M);
+  if (wis.found)
+    log_message(LOG_DEBUG, true, "Plan wisdom for %s M=%u: persist %d, FFT passes %d, HS stage %d\n", d.arch.c_str(),
+                d.plan.M, wis.persist_per_cu, wis.fft_passes, wis.hs_stage);
+  if (wis.persist_per_cu >= 0) d.persist_per_cu = static_cast<uint32_t>(wis.persist_per_cu);
   if (const char* e = std::getenv("BRP_PERSIST")) d.persist_per_cu = static_cast<uint32_t>(std::atoi(e));
+  d.hs_stage = wis.hs_stage >= 0 ? wis.hs_stage : 0;
+  if (const char* e = std::getenv("BRP_HS_STAGE")) d.hs_stage = std::atoi(e);
   d.plan.persist_wgs = d.persist_per_cu * d.num_cus;
   // opt-in (BRP_FFT2=1): measured 84 vs 78 us/template sequential, the
   // three-pass kernels keep more workgroups per CU (profiles/README.md)
-  d.two_pass = d.plan.M == hipk::kFft2M && 2ull * (hipk::kFft2L1 / 3) * hipk::kFft2R >= g.n_unpadded &&
-               std::getenv("BRP_FFT2") != nullptr;
+  const bool want2 = std::getenv("BRP_FFT2") ? std::atoi(std::getenv("BRP_FFT2")) != 0 : wis.fft_passes == 2;
+  d.two_pass = d.plan.M == hipk::kFft2M && 2ull * (hipk::kFft2L1 / 3) * hipk::kFft2R >= g.n_unpadded && want2;
   d.plan.legacy_pass1 = std::getenv("BRP_P1_LEGACY") != nullptr;
   d.plan.legacy_pass2 = std::getenv("BRP_P2_LEGACY") != nullptr;
   log_message(LOG_DEBUG, true, "FFT plan: N=%u M=%u = %u x %u x %u\n", g.nsamples, d.plan.M, d.plan.L1, d.plan.L2,
