@@ -212,6 +212,7 @@ def main() -> int:
             "data": data_desc,
             "recall_vs_golden": rec,
             "candidates_in_table": n_cands,
+            "collective_failure_degraded": ctx.degraded,
             "table_identical_to_warmup": (first == bytes(table.to_bytes())) if first is not None else None,
             "gpu_ms_rank0": round(stats["gpu_ms"], 3),
             "whiten_ms_rank0": round(stats["whiten_ms"], 3),

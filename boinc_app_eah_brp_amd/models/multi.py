@@ -35,20 +35,23 @@ class MultiWUSearch:
     def step(self, limit: int | None = None):
         """Whiten every WU, search this rank's share of the bank for all WUs,
         all-gather and merge. Returns one candidate table per WU."""
-        from ..parallel.dist import allgather_tables, merge_tables, shard_range
+        from ..parallel.dist import sharded_merge
 
         total = self.total if limit is None else min(limit, self.total)
-        begin, end = shard_range(total, self.ctx.rank, self.ctx.world)
         t0 = time.perf_counter()
         self.session.prepare()
         t1 = time.perf_counter()
-        tables, _ = self.session.run(begin, end)
-        t2 = time.perf_counter()
-        merged = []
-        for t in tables:
-            merged.append(merge_tables(allgather_tables(t, self.ctx)))
+        search_s = [0.0]
+
+        def run_shard(begin, end):
+            ts = time.perf_counter()
+            tables, _ = self.session.run(begin, end)
+            search_s[0] += time.perf_counter() - ts
+            return tables
+
+        merged = sharded_merge(run_shard, total, self.ctx)
         t3 = time.perf_counter()
-        for k, v in (("prepare", t1 - t0), ("templates", t2 - t1), ("merge", t3 - t2)):
+        for k, v in (("prepare", t1 - t0), ("templates", search_s[0]), ("merge", t3 - t1 - search_s[0])):
             self.timings[k] = self.timings.get(k, 0.0) + v
         return merged
 

@@ -1,3 +1,3 @@
 """Multi-GPU / multi-process parallelism (template-bank sharding over RCCL)."""
-from .dist import (DistContext, ShardedSearch, allgather_tables, barrier, init_distributed,  # noqa: F401
-                   max_over_ranks, merge_tables, shard_range)
+from .dist import (CollectiveError, DistContext, ShardedSearch, allgather_tables, barrier, degrade,  # noqa: F401
+                   init_distributed, max_over_ranks, merge_tables, shard_range, sharded_merge)

@@ -7,6 +7,13 @@ split instead: each rank processes a contiguous block of the template bank on
 its own GPU, and the per-rank 5x100 candidate tables (24 000 bytes each) are
 exchanged with ONE all-gather over xGMI and merged in rank order.
 
+Failure handling: every collective runs under
+BRP_COLLECTIVE_TIMEOUT seconds (default 600). When one fails or times out the
+rank aborts its process group, logs the failure and degrades to a single-GPU
+search: it computes the other ranks' shards itself, so rank 0 still writes the
+full, exact result. `BRP_FAULT=collective_timeout[:R]` makes rank R (default 1)
+stall before its first all-gather to exercise that path.
+
 The merge is exact: per harmonic level the sequential search
 keeps the 100 distinct bins with the largest maximum power, tagged with the
 first template reaching it, and `CandidateTable.merge` of tables ordered by
@@ -16,7 +23,10 @@ place, where the reference's qsort order is itself unspecified).
 from __future__ import annotations
 
 import os
+import sys
+import time
 from dataclasses import dataclass
+from datetime import timedelta
 
 import numpy as np
 
@@ -32,10 +42,30 @@ class DistContext:
     local_rank: int = 0
     backend: str = "none"
     device: object = None  # torch.device of the collectives
+    degraded: bool = False  # a collective failed: this rank now searches alone
+    stalled: bool = False   # the collective_timeout fault already fired
 
     @property
     def distributed(self) -> bool:
-        return self.world > 1
+        return self.world > 1 and not self.degraded
+
+
+class CollectiveError(RuntimeError):
+    """A collective failed or exceeded BRP_COLLECTIVE_TIMEOUT."""
+
+
+def collective_timeout_s() -> float:
+    return float(os.environ.get("BRP_COLLECTIVE_TIMEOUT", "600"))
+
+
+def fault_param(name: str) -> str | None:
+    """Parameter of `name` in BRP_FAULT ("" if given without one), None if absent
+    (same syntax as csrc/core/fault.hpp)."""
+    for tok in os.environ.get("BRP_FAULT", "").split(","):
+        key, _, arg = tok.partition(":")
+        if key == name:
+            return arg
+    return None
 
 
 def init_distributed(backend: str | None = None) -> DistContext:
@@ -60,7 +90,8 @@ def init_distributed(backend: str | None = None) -> DistContext:
         kwargs = {}
         if backend == "nccl":
             kwargs["device_id"] = dev
-        dist.init_process_group(backend=backend, rank=rank, world_size=world, **kwargs)
+        dist.init_process_group(backend=backend, rank=rank, world_size=world,
+                                timeout=timedelta(seconds=collective_timeout_s()), **kwargs)
     return DistContext(rank=rank, world=world, local_rank=local, backend=backend, device=dev)
 
 
@@ -82,14 +113,58 @@ def allgather_tables(table, ctx: DistContext) -> list:
     mine = torch.from_numpy(np.asarray(table.to_bytes(), dtype=np.uint8).copy())
     mine = mine.to(ctx.device)
     out = torch.empty(ctx.world * TABLE_BYTES, dtype=torch.uint8, device=ctx.device)
-    dist.all_gather_into_tensor(out, mine)
-    host = out.cpu().numpy()
+    stall = fault_param("collective_timeout")
+    if stall is not None and not ctx.stalled and ctx.rank == (int(stall) if stall else 1):
+        ctx.stalled = True
+        time.sleep(2 * collective_timeout_s() + 1)
+    try:
+        work = dist.all_gather_into_tensor(out, mine, async_op=True)
+        work.wait(timeout=timedelta(seconds=collective_timeout_s()))
+        host = out.cpu().numpy()
+    except Exception as e:  # gloo/RCCL timeout, peer gone, communicator error
+        raise CollectiveError(f"rank {ctx.rank}: table all-gather failed: {e}") from e
     tables = []
     for r in range(ctx.world):
         t = brp.CandidateTable()
         t.from_bytes(np.ascontiguousarray(host[r * TABLE_BYTES:(r + 1) * TABLE_BYTES]))
         tables.append(t)
     return tables
+
+
+def degrade(ctx: DistContext, err: Exception) -> None:
+    """Abort this rank's communicators and continue as a single-GPU search."""
+    print(f"[brp] WARNING: {err}; aborting the process group and continuing single-GPU", file=sys.stderr,
+          flush=True)
+    ctx.degraded = True
+    try:
+        import torch.distributed as dist
+        from torch.distributed import distributed_c10d as c10d
+
+        if hasattr(c10d, "_abort_process_group"):
+            c10d._abort_process_group()
+        else:
+            dist.destroy_process_group()
+    except Exception as e2:  # already torn down
+        print(f"[brp] process group teardown: {e2}", file=sys.stderr, flush=True)
+
+
+def sharded_merge(run_shard, total: int, ctx: DistContext) -> list:
+    """Search `total` templates split over the ranks and merge the tables.
+
+    run_shard(begin, end) returns one candidate table per work unit. If the
+    all-gather fails the rank degrades (see `degrade`) and runs the missing
+    shards itself, so the merged tables are the same either way."""
+    if not ctx.distributed:
+        return run_shard(0, total)
+    shards = [shard_range(total, r, ctx.world) for r in range(ctx.world)]
+    mine = run_shard(*shards[ctx.rank])
+    try:
+        gathered = [allgather_tables(t, ctx) for t in mine]
+    except CollectiveError as e:
+        degrade(ctx, e)
+        per_rank = [mine if r == ctx.rank else run_shard(*shards[r]) for r in range(len(shards))]
+        gathered = [[per_rank[r][w] for r in range(len(shards))] for w in range(len(mine))]
+    return [merge_tables(g) for g in gathered]
 
 
 def merge_tables(tables) -> object:
@@ -141,19 +216,21 @@ class ShardedSearch:
 
     def step(self, limit: int | None = None):
         """Whiten + search this rank's shard + all-gather + merge. Returns the merged table."""
-        import time
-
         total = self.total if limit is None else min(limit, self.total)
-        begin, end = shard_range(total, self.ctx.rank, self.ctx.world)
         t0 = time.perf_counter()
         self.session.prepare()
         t1 = time.perf_counter()
-        table, _ = self.session.run(begin, end, self.brp.CandidateTable())
-        t2 = time.perf_counter()
-        tables = allgather_tables(table, self.ctx)
-        merged = merge_tables(tables)
+        search_s = [0.0]
+
+        def run_shard(begin, end):
+            ts = time.perf_counter()
+            table, _ = self.session.run(begin, end, self.brp.CandidateTable())
+            search_s[0] += time.perf_counter() - ts
+            return [table]
+
+        merged = sharded_merge(run_shard, total, self.ctx)[0]
         t3 = time.perf_counter()
-        for k, v in (("prepare", t1 - t0), ("templates", t2 - t1), ("merge", t3 - t2)):
+        for k, v in (("prepare", t1 - t0), ("templates", search_s[0]), ("merge", t3 - t1 - search_s[0])):
             self.timings[k] = self.timings.get(k, 0.0) + v
         return merged
 

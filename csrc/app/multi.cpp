@@ -12,6 +12,7 @@
 #include "../core/errors.hpp"
 #include "../core/io.hpp"
 #include "../core/log.hpp"
+#include "../core/trace.hpp"
 #include "../engine/hip_engine.hpp"
 
 namespace brp {
@@ -111,6 +112,7 @@ int MultiSession::open(const std::vector<std::string>& inputs, const SearchOptio
 
 int MultiSession::prepare() {
   Impl& d = *impl_;
+  trace::Range range("brp:multi_prepare");
   const SearchGeometry& g = d.geoms[0];
   int rc;
   std::vector<std::vector<float>> prepared(d.wus.size());
@@ -144,6 +146,7 @@ int MultiSession::prepare() {
 
 int MultiSession::run(uint32_t begin, uint32_t end, std::vector<CandidateTable>& tables, MultiResult& res) {
   Impl& d = *impl_;
+  trace::Range range("brp:multi_templates");
   const SearchGeometry& g = d.geoms[0];
   const uint32_t K = static_cast<uint32_t>(d.wus.size());
   end = std::min<uint32_t>(end == 0 ? total() : end, total());

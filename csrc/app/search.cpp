@@ -17,6 +17,8 @@
 #include "../boinc/boinc_shim.hpp"
 #include "../boinc/ipc.hpp"
 #include "../core/errors.hpp"
+#include "../core/fault.hpp"
+#include "../core/trace.hpp"
 #include "../core/io.hpp"
 #include "../core/log.hpp"
 #include "../core/stats.hpp"
@@ -225,7 +227,10 @@ int SearchSession::open(const SearchOptions& opt, const SearchControl& ctl) {
       else if (dev < 0 && boinc::init_data().gpu_device_num >= 0) dev = boinc::init_data().gpu_device_num;
       int err = 0;
       b = make_hip_backend(dev, opt.batch, &err);
-      if (!b) return err ? err : RADPUL_HIP_DEVICE_FIND;
+      if (!b) {
+        boinc::end_critical_section();
+        return err ? err : RADPUL_HIP_DEVICE_FIND;
+      }
     }
     d.backends.push_back(std::move(b));
   }
@@ -235,10 +240,14 @@ int SearchSession::open(const SearchOptions& opt, const SearchControl& ctl) {
 
 int SearchSession::prepare() {
   Impl& d = *impl_;
+  trace::Range range("brp:prepare");
   d.series = d.wu.samples;
   boinc::begin_critical_section();
   int rc = d.backends[0]->setup(d.g, d.opt, d.series, d.zaps);
-  if (rc) return rc;
+  if (rc) {
+    boinc::end_critical_section();
+    return rc;
+  }
   SearchOptions opt_nw = d.opt;
   opt_nw.white = false;
   opt_nw.prewhitened = d.opt.white;
@@ -248,7 +257,10 @@ int SearchSession::prepare() {
   for (size_t k = 1; k < d.backends.size(); ++k) {
     std::vector<float> s = d.series;
     rc = d.backends[k]->setup(d.g, opt_nw, s, d.zaps);
-    if (rc) return rc;
+    if (rc) {
+      boinc::end_critical_section();
+      return rc;
+    }
   }
   boinc::end_critical_section();
   return 0;
@@ -257,6 +269,7 @@ int SearchSession::prepare() {
 int SearchSession::run(uint32_t begin, uint32_t end, CandidateTable& table, SearchResult& res,
                        const TemplateHook& hook) {
   Impl& d = *impl_;
+  trace::Range range("brp:templates");
   const SearchGeometry& g = d.g;
   end = std::min<uint32_t>(end, total());
   if (begin >= end) return 0;
@@ -426,9 +439,9 @@ int run_search(const SearchOptions& opt, const SearchControl& ctl, SearchResult&
   res.t_setup = now_s() - t_start;
 
   const double t_loop = now_s();
-  const char* fault = std::getenv("BRP_FAULT");
   long kill_after = -1;
-  if (fault && std::strncmp(fault, "kill_after_template:", 20) == 0) kill_after = std::atol(fault + 20);
+  std::string fault_arg;
+  if (fault_enabled("kill_after_template", &fault_arg)) kill_after = std::atol(fault_arg.c_str());
   int cp_rc = 0;
   auto hook = [&](uint32_t done, const SearchInfo& info) -> bool {
     counter = done;
@@ -441,6 +454,7 @@ int run_search(const SearchOptions& opt, const SearchControl& ctl, SearchResult&
       cp.header.n_template = counter;
       std::snprintf(cp.header.originalfile, sizeof(cp.header.originalfile), "%s", opt.inputfile.c_str());
       std::memcpy(cp.cands, table.data(), sizeof(cp.cands));
+      trace::Range range("brp:checkpoint");
       cp_rc = write_checkpoint(opt.checkpointfile, cp);
       if (cp_rc) return false;
       log_message(LOG_INFO, true, "Checkpoint committed!\n");
@@ -464,6 +478,7 @@ int run_search(const SearchOptions& opt, const SearchControl& ctl, SearchResult&
   }
   if (ctl.write_output) {
     log_message(LOG_DEBUG, true, "Search done!\n");
+    trace::Range range("brp:finalize_output");
     rc = finalize_output(opt, g, counter, table, "einsteinbinary_mi355x");
     if (rc) return rc;
   }

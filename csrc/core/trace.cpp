@@ -1,0 +1,66 @@
+#include "trace.hpp"
+
+#include <dlfcn.h>
+
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+
+#include "log.hpp"
+
+namespace brp {
+namespace trace {
+namespace {
+
+struct Roctx {
+  int (*push)(const char*) = nullptr;
+  int (*pop)() = nullptr;
+  void (*mark)(const char*) = nullptr;
+  bool on = false;
+};
+
+const Roctx& roctx() {
+  static Roctx r;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    const char* env = std::getenv("BRP_ROCTX");
+    if (!env || !*env || std::strcmp(env, "0") == 0) return;
+    const char* libs[] = {"librocprofiler-sdk-roctx.so.1", "librocprofiler-sdk-roctx.so", "libroctx64.so.4",
+                          "libroctx64.so"};
+    void* h = nullptr;
+    for (const char* l : libs)
+      if ((h = dlopen(l, RTLD_NOW | RTLD_GLOBAL))) break;
+    if (!h) {
+      log_message(LOG_WARN, true, "BRP_ROCTX set but no roctx library could be loaded: %s\n", dlerror());
+      return;
+    }
+    r.push = reinterpret_cast<int (*)(const char*)>(dlsym(h, "roctxRangePushA"));
+    r.pop = reinterpret_cast<int (*)()>(dlsym(h, "roctxRangePop"));
+    r.mark = reinterpret_cast<void (*)(const char*)>(dlsym(h, "roctxMarkA"));
+    r.on = r.push && r.pop;
+    if (r.on) log_message(LOG_DEBUG, true, "roctx ranges enabled.\n");
+  });
+  return r;
+}
+
+}  // namespace
+
+bool enabled() { return roctx().on; }
+
+void range_push(const char* name) {
+  const Roctx& r = roctx();
+  if (r.on) r.push(name);
+}
+
+void range_pop() {
+  const Roctx& r = roctx();
+  if (r.on) r.pop();
+}
+
+void mark(const char* name) {
+  const Roctx& r = roctx();
+  if (r.on && r.mark) r.mark(name);
+}
+
+}  // namespace trace
+}  // namespace brp

@@ -18,6 +18,8 @@
 #include <unordered_map>
 
 #include "../core/errors.hpp"
+#include "../core/fault.hpp"
+#include "../core/trace.hpp"
 #include "../core/gsl_compat.hpp"
 #include "../core/cpu_backend.hpp"
 #include "../core/log.hpp"
@@ -76,8 +78,9 @@ struct DevBuf {
   int alloc(size_t count) {
     release();
     if (count == 0) return 0;
-    if (hipMalloc(&p, count * sizeof(T)) != hipSuccess) {
+    if (fault_enabled("hip_oom") || hipMalloc(&p, count * sizeof(T)) != hipSuccess) {
       p = nullptr;
+      log_message(LOG_ERROR, true, "Couldn't allocate %zu bytes of device memory!\n", count * sizeof(T));
       return RADPUL_HIP_MEM_ALLOC_DEVICE;
     }
     n = count;
@@ -95,20 +98,34 @@ template <typename T>
 struct PinnedBuf {
   T* p = nullptr;
   size_t n = 0;
+  bool pageable = false;
+  // Pinned first; if the runtime refuses (locked-memory limits), fall back to
+  // pageable memory like the reference's HS host buffers
+  // (cuda/app/demod_binary_hs_cuda.cu:207-219): copies then stage through the
+  // runtime's own pinned bounce buffers, slower but correct.
   int alloc(size_t count) {
     release();
     if (count == 0) return 0;
-    if (hipHostMalloc(&p, count * sizeof(T), hipHostMallocDefault) != hipSuccess) {
-      p = nullptr;
-      return RADPUL_HIP_MEM_ALLOC_HOST;
+    if (fault_enabled("pinned_fail") || hipHostMalloc(&p, count * sizeof(T), hipHostMallocDefault) != hipSuccess) {
+      p = static_cast<T*>(std::malloc(count * sizeof(T)));
+      if (!p) return RADPUL_HIP_MEM_ALLOC_HOST;
+      pageable = true;
+      log_message(LOG_WARN, true, "Couldn't allocate %zu bytes of pinned host memory, using pageable memory.\n",
+                  count * sizeof(T));
     }
     n = count;
     return 0;
   }
   void release() {
-    if (p) (void)hipHostFree(p);
+    if (p) {
+      if (pageable)
+        std::free(p);
+      else
+        (void)hipHostFree(p);
+    }
     p = nullptr;
     n = 0;
+    pageable = false;
   }
   ~PinnedBuf() { release(); }
 };
@@ -495,6 +512,7 @@ bool same_geometry(const SearchGeometry& a, const SearchGeometry& b) {
 }  // namespace
 
 int HipEngine::setup(const SearchGeometry& g, const std::vector<float>& series, float mu0) {
+  trace::Range range("brp:engine_setup");
   Impl& d = *impl_;
   BRP_HIP_CHECK(hipSetDevice(d.device), RADPUL_HIP_DEVICE_SET);
   if (d.ready && same_geometry(d.g, g)) {
@@ -766,6 +784,7 @@ int HipEngine::process(const TemplateInput* t, int n, const float* thr, int thr_
   const SearchGeometry& g = d.g;
   for (int off = 0; off < n; off += d.batch) {
     const int nb = std::min(d.batch, n - off);
+    trace::range_push("brp:batch_launch");
     for (int k = 0; k < nb; ++k) {
       TemplateDev td{};
       td.p = make_resamp_params(g.nsamples, g.n_unpadded, g.fft_size, g.dt, g.step_inv, t[off + k].P,
@@ -805,7 +824,12 @@ int HipEngine::process(const TemplateInput* t, int n, const float* thr, int thr_
       BRP_HIP_CHECK(d.enqueue(nb), RADPUL_HIP_KERNEL_INVOKE);
     }
     BRP_HIP_CHECK(hipEventRecord(d.ev1, d.stream), RADPUL_HIP_KERNEL_INVOKE);
-    BRP_HIP_CHECK(hipStreamSynchronize(d.stream), RADPUL_HIP_KERNEL_INVOKE);
+    trace::range_pop();
+    {
+      trace::Range wait("brp:batch_wait");
+      BRP_HIP_CHECK(hipStreamSynchronize(d.stream), RADPUL_HIP_KERNEL_INVOKE);
+    }
+    trace::Range decode("brp:batch_decode");
     float ms = 0;
     (void)hipEventElapsedTime(&ms, d.ev0, d.ev1);
     d.st.gpu_ms += ms;
@@ -902,8 +926,6 @@ int HipEngine::power_spectrum(const TemplateInput& t, std::vector<float>& ps_out
     ps_out.resize(g.fft_size);
     BRP_HIP_CHECK(hipMemcpyAsync(ps_out.data(), full.p, g.fft_size * sizeof(float), hipMemcpyDeviceToHost, s),
                   RADPUL_HIP_MEM_COPY_DEVICE_HOST);
-    BRP_HIP_CHECK(hipMemcpyAsync(d.h_tmpl.p, d.tmpl.p, sizeof(TemplateDev), hipMemcpyDeviceToHost, s),
-                  RADPUL_HIP_MEM_COPY_DEVICE_HOST);
     BRP_HIP_CHECK(hipStreamSynchronize(s), RADPUL_HIP_KERNEL_INVOKE);
     if (n_steps) *n_steps = d.h_tmpl.p[0].n_steps;
     return 0;
@@ -953,8 +975,6 @@ int HipEngine::power_spectrum(const TemplateInput& t, std::vector<float>& ps_out
   ps_out.resize(g.fft_size);
   BRP_HIP_CHECK(hipMemcpyAsync(ps_out.data(), full.p, g.fft_size * sizeof(float), hipMemcpyDeviceToHost, s),
                 RADPUL_HIP_MEM_COPY_DEVICE_HOST);
-  BRP_HIP_CHECK(hipMemcpyAsync(d.h_tmpl.p, d.tmpl.p, sizeof(TemplateDev), hipMemcpyDeviceToHost, s),
-                RADPUL_HIP_MEM_COPY_DEVICE_HOST);
   BRP_HIP_CHECK(hipStreamSynchronize(s), RADPUL_HIP_KERNEL_INVOKE);
   if (n_steps) *n_steps = d.h_tmpl.p[0].n_steps;
   return 0;
@@ -993,7 +1013,12 @@ int HipEngine::benchmark_stages(const TemplateInput* t, int n, int reps, std::ve
       }
     }
     BRP_HIP_CHECK(hipEventRecord(d.ev1, d.stream), RADPUL_HIP_KERNEL_INVOKE);
-    BRP_HIP_CHECK(hipStreamSynchronize(d.stream), RADPUL_HIP_KERNEL_INVOKE);
+    trace::range_pop();
+    {
+      trace::Range wait("brp:batch_wait");
+      BRP_HIP_CHECK(hipStreamSynchronize(d.stream), RADPUL_HIP_KERNEL_INVOKE);
+    }
+    trace::Range decode("brp:batch_decode");
     float ms = 0;
     (void)hipEventElapsedTime(&ms, d.ev0, d.ev1);
     us_per_launch[st] = 1e3 * ms / reps;

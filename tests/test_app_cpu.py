@@ -195,3 +195,27 @@ def test_app_mi355x_flags_parse(app, case, tmp_path):
     (tmp_path / "c").mkdir()
     r2 = _run_app(app, _app_args(case, tmp_path / "c", ["--mi355x-ps-fp16", "-h"]), tmp_path)
     assert "--mi355x-spin" in r2.stdout + r2.stderr
+
+
+def test_app_roctx_ranges_do_not_change_results(app, case, tmp_path):
+    """BRP_ROCTX=1 loads the roctx library (dlopen) and brackets the host phases;
+    the result file is unchanged."""
+    a, b = tmp_path / "a", tmp_path / "b"
+    a.mkdir()
+    b.mkdir()
+    r1 = _run_app(app, _app_args(case, a), a)
+    r2 = _run_app(app, _app_args(case, b), b, BRP_ROCTX="1")
+    assert r1.returncode == 0 and r2.returncode == 0, r2.stderr[-2000:]
+    assert (a / "res.cand").read_text() == (b / "res.cand").read_text()
+
+
+def test_fault_spec_parsing(monkeypatch):
+    from boinc_app_eah_brp_amd.parallel.dist import fault_param
+
+    monkeypatch.setenv("BRP_FAULT", "hip_oom,collective_timeout:3,kill_after_template:9")
+    assert fault_param("collective_timeout") == "3"
+    assert fault_param("hip_oom") == ""
+    assert fault_param("kill_after_template") == "9"
+    assert fault_param("kill_after") is None
+    monkeypatch.delenv("BRP_FAULT")
+    assert fault_param("hip_oom") is None

@@ -40,3 +40,18 @@ def test_bench_multirank_cpu_rehearsal(nproc, tmp_path):
     assert many["value"] > 0 and many["config"]["parallelism"].startswith(f"dp{nproc}")
     assert many["table_identical_to_warmup"] is True
     assert (tmp_path / "one.cand").read_text() == (tmp_path / "many.cand").read_text()
+
+
+def test_collective_timeout_degrades_to_single_gpu(tmp_path):
+    """BRP_FAULT=collective_timeout:1 stalls rank 1 before the all-gather; rank 0
+    times out, aborts the process group, searches the missing shard itself and
+    writes the same result file as an undisturbed run."""
+    one = _bench(1, tmp_path / "w1", tmp_path / "one.cand")
+    os.environ["BRP_FAULT"], os.environ["BRP_COLLECTIVE_TIMEOUT"] = "collective_timeout:1", "3"
+    try:
+        two = _bench(2, tmp_path / "w2", tmp_path / "two.cand")
+    finally:
+        del os.environ["BRP_FAULT"], os.environ["BRP_COLLECTIVE_TIMEOUT"]
+    assert one["collective_failure_degraded"] is False
+    assert two["collective_failure_degraded"] is True
+    assert (tmp_path / "one.cand").read_text() == (tmp_path / "two.cand").read_text()

@@ -173,3 +173,32 @@ def test_fp16_power_spectrum_config(brp, gpu, case, tmp_path):
     with pytest.raises(RuntimeError):
         BRPSearch(_cfg(case, tmp_path / "c", ps_fp16=True, white=False)).run(write_output=False,
                                                                            use_checkpoint=False)
+
+
+def _app_gpu(case, d, **env):
+    d = Path(d)
+    d.mkdir(parents=True, exist_ok=True)
+    args = ["-i", case["wu"], "-t", case["bank"], "-l", case["zap"], "-o", str(d / "res.cand"), "-c",
+            str(d / "cp.cpt"), "-A", "0.08", "-P", "3.0", "-f", "400.0", "-W", "-B", "100"]
+    e = dict(os.environ, BRP_NO_RESULT_HEADER="1", **env)
+    return subprocess.run([str(app_binary()), *args], cwd=d, env=e, capture_output=True, text=True, timeout=300)
+
+
+def test_fault_hip_oom_temporary_exit(brp, gpu, case, tmp_path):
+    """Device allocation failure -> BOINC temporary exit, no result written
+    (erp_boinc_wrapper.cpp:560-570)."""
+    r = _app_gpu(case, tmp_path, BRP_FAULT="hip_oom")
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "Temporary exit (900 s)" in r.stderr, r.stderr[-3000:]
+    assert "device memory" in r.stderr
+    assert not (tmp_path / "res.cand").exists()
+
+
+def test_fault_pinned_fail_falls_back_to_pageable(brp, gpu, case, tmp_path):
+    """Pinned host allocation failure -> pageable buffers, identical results
+    (cuda/app/demod_binary_hs_cuda.cu:207-219)."""
+    a = _app_gpu(case, tmp_path / "a")
+    b = _app_gpu(case, tmp_path / "b", BRP_FAULT="pinned_fail")
+    assert a.returncode == 0 and b.returncode == 0, b.stderr[-3000:]
+    assert "pageable" in b.stderr
+    assert (tmp_path / "a" / "res.cand").read_bytes() == (tmp_path / "b" / "res.cand").read_bytes()
