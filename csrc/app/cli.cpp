@@ -45,6 +45,8 @@ void print_usage(const char* prog) {
   std::printf(" --mi355x-ps-fp16\t\tboolean\tStore the power spectrum as fp16 (needs -W).\n");
   std::printf(" --mi355x-spin\t\t\tboolean\tBusy-wait for the GPU instead of sleeping (default: blocking sync).\n");
   std::printf(" --mi355x-pipelines\t\tinteger\tIndependent pipelines per GPU (default 3, one template each).\n");
+  std::printf(" --mi355x-no-checkpoint\t\tboolean\tNever read or write checkpoints (Debian NOCHECKPOINTING build).\n");
+  std::printf(" --mi355x-progress-every\tinteger\tReport fraction done every N templates (Debian COMMUNICATIONREDUCTION).\n");
   std::printf("\n");
 }
 
@@ -179,6 +181,16 @@ int search_main(int argc, char** argv) {
       if (!v) return RADPUL_EVAL;
       ctl.pipelines = std::max(1, std::atoi(v));
       i += 2;
+    } else if (std::strcmp(a, "--mi355x-no-checkpoint") == 0) {
+      // runtime form of the Debian package's -DNOCHECKPOINTING
+      // (debian/patches/disable_checkpointing.patch)
+      ctl.use_checkpoint = false;
+      i++;
+    } else if (std::strcmp(a, "--mi355x-progress-every") == 0) {
+      // runtime form of -DCOMMUNICATIONREDUCTION=N (debian/patches/progressfraction.patch)
+      if (!v) return RADPUL_EVAL;
+      ctl.progress_every = static_cast<uint32_t>(std::max(1, std::atoi(v)));
+      i += 2;
     } else if (std::strcmp(a, "--mi355x-ps-fp16") == 0) {
       opt.ps_fp16 = true;
       i++;
@@ -195,6 +207,10 @@ int search_main(int argc, char** argv) {
       log_message(LOG_ERROR, true, "\nUnknown option \"%s\". Use '%s --help'.\n\n", a, argv[0]);
       return RADPUL_EMISC;
     }
+  }
+  if (!ctl.use_checkpoint && !opt.checkpointfile.empty()) {
+    log_message(LOG_ERROR, true, "Disabled checkpointing - '-c %s' option ignored\n", opt.checkpointfile.c_str());
+    opt.checkpointfile.clear();
   }
   // a BOINC app shares the host: wait for the GPU by sleeping, as the
   // reference's blocking-sync context does, unless --mi355x-spin
@@ -235,6 +251,8 @@ int wrapper_main(int argc, char** argv) {
                                          {"mi355x-ps-fp16", no_argument, 0, 1004},
                                          {"mi355x-spin", no_argument, 0, 1005},
                                          {"mi355x-pipelines", required_argument, 0, 1006},
+                                         {"mi355x-no-checkpoint", no_argument, 0, 1007},
+                                         {"mi355x-progress-every", required_argument, 0, 1008},
                                          {0, 0, 0, 0}};
   optind = 1;
   auto file_arg = [&](const char* opt, const char* val) {
@@ -276,6 +294,8 @@ int wrapper_main(int argc, char** argv) {
       case 1004: fwd.push_back("--mi355x-ps-fp16"); break;
       case 1005: fwd.push_back("--mi355x-spin"); break;
       case 1006: fwd.push_back("--mi355x-pipelines"); fwd.push_back(optarg); break;
+      case 1007: fwd.push_back("--mi355x-no-checkpoint"); break;
+      case 1008: fwd.push_back("--mi355x-progress-every"); fwd.push_back(optarg); break;
       default: boinc::finish(EINSTEINRADIO_EOPT);
     }
   }

@@ -445,8 +445,10 @@ int run_search(const SearchOptions& opt, const SearchControl& ctl, SearchResult&
   int cp_rc = 0;
   auto hook = [&](uint32_t done, const SearchInfo& info) -> bool {
     counter = done;
-    if (ipc::update_due()) ipc::update_shmem(info);
-    boinc::fraction_done((counter + 1.0) / total);
+    if (ctl.progress_every <= 1 || counter % ctl.progress_every == 0) {
+      if (ipc::update_due()) ipc::update_shmem(info);
+      boinc::fraction_done((counter + 1.0) / total);
+    }
     if (ctl.on_template) ctl.on_template(counter, total);
     if (ctl.use_checkpoint && !opt.checkpointfile.empty() && boinc::time_to_checkpoint()) {
       Checkpoint cp;

@@ -32,6 +32,7 @@ struct SearchControl {
   bool use_checkpoint = true;
   int gpus = 1;                   // devices driven by this process (in-order merge)
   int pipelines = 1;              // independent pipelines (stream + buffers) per device
+  uint32_t progress_every = 1;    // fraction_done / screensaver every N templates
   std::vector<int> devices;       // explicit device ids (optional)
   // called after every template applied (progress hooks / fault injection)
   std::function<void(uint32_t done, uint32_t total)> on_template;

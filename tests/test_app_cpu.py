@@ -219,3 +219,22 @@ def test_fault_spec_parsing(monkeypatch):
     assert fault_param("kill_after") is None
     monkeypatch.delenv("BRP_FAULT")
     assert fault_param("hip_oom") is None
+
+
+def test_app_no_checkpoint_and_progress_every(app, case, tmp_path):
+    """--mi355x-no-checkpoint (Debian -DNOCHECKPOINTING) never writes a checkpoint,
+    even when interrupted; --mi355x-progress-every (-DCOMMUNICATIONREDUCTION)
+    leaves the results unchanged."""
+    ref, run, cut = tmp_path / "ref", tmp_path / "run", tmp_path / "cut"
+    for d in (ref, run, cut):
+        d.mkdir()
+    r = _run_app(app, _app_args(case, ref), ref)
+    assert r.returncode == 0, r.stderr[-2000:]
+    extra = ("--mi355x-no-checkpoint", "--mi355x-progress-every", "5")
+    r = _run_app(app, _app_args(case, run, extra), run, BRP_CHECKPOINT_PERIOD="0")
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "option ignored" in r.stderr
+    assert _result_lines(run / "res.cand") == _result_lines(ref / "res.cand")
+    r = _run_app(app, _app_args(case, cut, extra), cut, BRP_CHECKPOINT_PERIOD="0", BRP_FAULT="kill_after_template:5")
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert not (cut / "cp.cpt").exists() and not (cut / "res.cand").exists()

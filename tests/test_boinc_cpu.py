@@ -90,3 +90,16 @@ def test_help_and_bad_values(app, small, tmp_path):
     for bad in (["-P", "0.5"], ["-P", "11"], ["-A", "2"], ["-f", "-1"], ["-B", "-3"]):
         r = _run(app, _args(small, tmp_path / "r.cand", tmp_path / "c.cpt", bad), tmp_path)
         assert r.returncode != 0, bad
+
+
+def test_app_info_template_is_valid():
+    """data/boinc/app_info.xml.in (anonymous-platform descriptor) is well formed
+    and names an AMD GPU coprocessor and options the application accepts."""
+    import xml.etree.ElementTree as ET
+    from pathlib import Path
+
+    root = ET.parse(Path(__file__).resolve().parent.parent / "data" / "boinc" / "app_info.xml.in").getroot()
+    av = root.find("app_version")
+    assert av.find("coproc/type").text == "ATI"
+    assert av.find("file_ref/file_name").text == root.find("file_info/name").text
+    assert av.find("cmdline").text.split()[0] == "--mi355x-pipelines"
