@@ -10,11 +10,13 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <string>
 #include <unordered_map>
 
 #include "../core/errors.hpp"
@@ -75,10 +77,15 @@ template <typename T>
 struct DevBuf {
   T* p = nullptr;
   size_t n = 0;
-  int alloc(size_t count) {
+  // fine: fine-grained device memory the host can read and write in place
+  // (over the PCIe BAR) -- used for the per-batch parameters and results
+  int alloc(size_t count, bool fine = false) {
     release();
     if (count == 0) return 0;
-    if (fault_enabled("hip_oom") || hipMalloc(&p, count * sizeof(T)) != hipSuccess) {
+    const hipError_t e = fine ? hipExtMallocWithFlags(reinterpret_cast<void**>(&p), count * sizeof(T),
+                                                      hipDeviceMallocFinegrained)
+                              : hipMalloc(&p, count * sizeof(T));
+    if (fault_enabled("hip_oom") || e != hipSuccess) {
       p = nullptr;
       log_message(LOG_ERROR, true, "Couldn't allocate %zu bytes of device memory!\n", count * sizeof(T));
       return RADPUL_HIP_MEM_ALLOC_DEVICE;
@@ -117,7 +124,7 @@ struct PinnedBuf {
     return 0;
   }
   void release() {
-    if (p) {
+    if (p && n) {  // n == 0: a non-owning view
       if (pageable)
         std::free(p);
       else
@@ -129,6 +136,27 @@ struct PinnedBuf {
   }
   ~PinnedBuf() { release(); }
 };
+
+// A fine-grained device allocation the host may read and write in place: on
+// a large-BAR device (all MI355X platforms) ROCm maps device memory into the
+// host address space at the same address. Checked with a host-written pattern
+// read back through a device copy.
+void* host_view(int device, void* p, size_t bytes) {
+  int large_bar = 0;
+  if (hipDeviceGetAttribute(&large_bar, hipDeviceAttributeIsLargeBar, device) != hipSuccess) return nullptr;
+  hipPointerAttribute_t at{};
+  if (hipPointerGetAttributes(&at, p) != hipSuccess) return nullptr;
+  void* h = at.hostPointer != nullptr ? at.hostPointer : p;
+  log_message(LOG_DEBUG, true, "fine-grained buffer %p: large BAR %d, host pointer %p -> %p\n", p, large_bar,
+              at.hostPointer, h);
+  if (!large_bar) return nullptr;
+  std::vector<uint8_t> pat(bytes), back(bytes);
+  for (size_t i = 0; i < bytes; ++i) pat[i] = static_cast<uint8_t>(i * 37u + 11u);
+  std::memcpy(h, pat.data(), bytes);
+  std::atomic_thread_fence(std::memory_order_seq_cst);
+  if (hipMemcpy(back.data(), p, bytes, hipMemcpyDeviceToHost) != hipSuccess) return nullptr;
+  return pat == back ? h : nullptr;
+}
 
 // W_{2N}^j = exp(-i pi j / N) as a two-level float table
 void build_twiddles(uint64_t period, std::vector<float2>& hi, std::vector<float2>& lo) {
@@ -184,6 +212,10 @@ struct HipEngine::Impl {
   // two-pass template FFT (fft2.hip) for the 3x-padded production shape
   // M = 768 * 8192; the three-pass plan stays in use for whitening
   bool two_pass = false;
+  // per-batch parameters / candidate results in fine-grained device memory the
+  // host writes / reads directly, instead of two small copies per batch
+  // (each a runtime blit kernel on the GPU); BRP_FG=in|out|both|0
+  bool fg_in = false, fg_out = false;
 
   DevBuf<float> series;
   DevBuf<float2> buf;           // [batch][M]
@@ -305,6 +337,7 @@ struct HipEngine::Impl {
       case kPrologue:
         // n_steps comes with the parameters (host bracketed search); pass 1
         // zeroes the batch's candidate counter
+        if (fg_in) return hipSuccess;  // the host wrote `in` directly
         return hipMemcpyAsync(in.p, h_in.p, thr_bytes + sizeof(TemplateDev) * nb, hipMemcpyHostToDevice, stream);
       case kPass1: {
         if (two_pass) {
@@ -413,6 +446,7 @@ struct HipEngine::Impl {
         return hipk::launch_harmonic_sum(ah, nb, stream);
       }
       case kEpilogue:
+        if (fg_out) return hipSuccess;  // the host reads `cands` directly
         return hipMemcpyAsync(h_cands.p, cands.p, sizeof(uint2) * (1 + kcopy), hipMemcpyDeviceToHost, stream);
       default: return hipErrorInvalidValue;
     }
@@ -578,14 +612,43 @@ int HipEngine::setup(const SearchGeometry& g, const std::vector<float>& series, 
   }
   d.thr_bytes = (B * hipk::kHsThrStride * sizeof(float) + 63) / 64 * 64;
   const size_t in_bytes = d.thr_bytes + sizeof(TemplateDev) * B;
-  if ((rc = d.in.alloc(in_bytes))) return rc;
+  {
+    const char* fg = std::getenv("BRP_FG");
+    const std::string f = fg ? fg : "";
+    // measured (profiles/README.md): parameters in place +1.9%, results in
+    // place +0.8%; default "in"
+    d.fg_in = f.empty() || f == "in" || f == "both" || f == "1";
+    d.fg_out = f == "out" || f == "both" || f == "1";
+  }
+  if ((rc = d.in.alloc(in_bytes, d.fg_in))) return rc;
+  uint8_t* in_host = d.fg_in ? static_cast<uint8_t*>(host_view(d.device, d.in.p, in_bytes)) : nullptr;
+  if (d.fg_in && in_host == nullptr) {
+    log_message(LOG_WARN, true, "Fine-grained device memory is not host visible; copying the batch parameters.\n");
+    d.fg_in = false;
+    if ((rc = d.in.alloc(in_bytes))) return rc;
+  }
   d.thr.p = reinterpret_cast<float*>(d.in.p);
   d.tmpl.p = reinterpret_cast<TemplateDev*>(d.in.p + d.thr_bytes);
-  if ((rc = d.cands.alloc(1 + d.cap))) return rc;
-  if ((rc = d.h_in.alloc(in_bytes))) return rc;
-  d.h_thr.p = reinterpret_cast<float*>(d.h_in.p);
-  d.h_tmpl.p = reinterpret_cast<TemplateDev*>(d.h_in.p + d.thr_bytes);
-  if ((rc = d.h_cands.alloc(1 + d.kcopy))) return rc;
+  if ((rc = d.cands.alloc(1 + d.cap, d.fg_out))) return rc;
+  if (d.fg_in) {
+    d.h_thr.p = reinterpret_cast<float*>(in_host);
+    d.h_tmpl.p = reinterpret_cast<TemplateDev*>(in_host + d.thr_bytes);
+  } else {
+    if ((rc = d.h_in.alloc(in_bytes))) return rc;
+    d.h_thr.p = reinterpret_cast<float*>(d.h_in.p);
+    d.h_tmpl.p = reinterpret_cast<TemplateDev*>(d.h_in.p + d.thr_bytes);
+  }
+  uint2* cands_host = d.fg_out ? static_cast<uint2*>(host_view(d.device, d.cands.p, sizeof(uint2) * (1 + d.kcopy))) : nullptr;
+  if (d.fg_out && cands_host == nullptr) {
+    log_message(LOG_WARN, true, "Fine-grained device memory is not host visible; copying the results.\n");
+    d.fg_out = false;
+    if ((rc = d.cands.alloc(1 + d.cap))) return rc;
+  }
+  if (d.fg_out) {
+    d.h_cands.p = cands_host;  // non-owning view (PinnedBuf::n stays 0)
+  } else if ((rc = d.h_cands.alloc(1 + d.kcopy))) {
+    return rc;
+  }
   std::vector<float2> hi, lo;
   build_twiddles(4ull * d.plan.M, hi, lo);
   if ((rc = d.tw_hi.alloc(hi.size()))) return rc;
@@ -817,6 +880,7 @@ int HipEngine::process(const TemplateInput* t, int n, const float* thr, int thr_
         exec = it->second;
       }
     }
+    if (d.fg_in) std::atomic_thread_fence(std::memory_order_seq_cst);  // BAR writes before the launch
     BRP_HIP_CHECK(hipEventRecord(d.ev0, d.stream), RADPUL_HIP_KERNEL_INVOKE);
     if (use_graph) {
       BRP_HIP_CHECK(hipGraphLaunch(exec, d.stream), RADPUL_HIP_GRAPH);
@@ -880,8 +944,10 @@ int HipEngine::power_spectrum(const TemplateInput& t, std::vector<float>& ps_out
   td.n_steps = resamp_n_steps(td.p, kSinLut, kCosLut);
   d.h_tmpl.p[0] = td;
   hipStream_t s = d.stream;
-  BRP_HIP_CHECK(hipMemcpyAsync(d.tmpl.p, d.h_tmpl.p, sizeof(TemplateDev), hipMemcpyHostToDevice, s),
-                RADPUL_HIP_MEM_COPY_HOST_DEVICE);
+  if (!d.fg_in)
+    BRP_HIP_CHECK(hipMemcpyAsync(d.tmpl.p, d.h_tmpl.p, sizeof(TemplateDev), hipMemcpyHostToDevice, s),
+                  RADPUL_HIP_MEM_COPY_HOST_DEVICE);
+  std::atomic_thread_fence(std::memory_order_seq_cst);
   const hipk::TwiddleTable tw = d.twt();
   if (d.two_pass) {
     // the template pipeline's transform: pass A, pass B, transpose (all bins)
@@ -993,6 +1059,7 @@ int HipEngine::benchmark_stages(const TemplateInput* t, int n, int reps, std::ve
     d.h_tmpl.p[k] = td;
     for (int h = 0; h < kNumHarmonicLevels; ++h) d.h_thr.p[k * hipk::kHsThrStride + h] = d.g.chi2_thr[h];
   }
+  std::atomic_thread_fence(std::memory_order_seq_cst);
   BRP_HIP_CHECK(d.enqueue(nb), RADPUL_HIP_KERNEL_INVOKE);
   BRP_HIP_CHECK(hipStreamSynchronize(d.stream), RADPUL_HIP_KERNEL_INVOKE);
   us_per_launch.assign(Impl::kNumStages + 1, 0.0);

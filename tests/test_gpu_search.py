@@ -197,8 +197,22 @@ def test_fault_hip_oom_temporary_exit(brp, gpu, case, tmp_path):
 def test_fault_pinned_fail_falls_back_to_pageable(brp, gpu, case, tmp_path):
     """Pinned host allocation failure -> pageable buffers, identical results
     (cuda/app/demod_binary_hs_cuda.cu:207-219)."""
-    a = _app_gpu(case, tmp_path / "a")
-    b = _app_gpu(case, tmp_path / "b", BRP_FAULT="pinned_fail")
+    a = _app_gpu(case, tmp_path / "a", BRP_FG="0")
+    b = _app_gpu(case, tmp_path / "b", BRP_FAULT="pinned_fail", BRP_FG="0")
     assert a.returncode == 0 and b.returncode == 0, b.stderr[-3000:]
     assert "pageable" in b.stderr
     assert (tmp_path / "a" / "res.cand").read_bytes() == (tmp_path / "b" / "res.cand").read_bytes()
+
+
+def test_fine_grained_parameter_and_result_buffers(brp, gpu, case, tmp_path):
+    """Batch parameters / candidate lists in host-visible fine-grained device
+    memory (BRP_FG, default "in") give the same result file as the copy path."""
+    runs = {}
+    for fg in ("0", "in", "out", "both"):
+        r = _app_gpu(case, tmp_path / fg, BRP_FG=fg, BRP_LOGLEVEL="4")
+        assert r.returncode == 0, r.stderr[-3000:]
+        assert "not host visible" not in r.stderr, r.stdout[-2000:]
+        if fg != "0":
+            assert "large BAR 1" in r.stdout + r.stderr
+        runs[fg] = (tmp_path / fg / "res.cand").read_bytes()
+    assert runs["in"] == runs["0"] and runs["out"] == runs["0"] and runs["both"] == runs["0"]
