@@ -206,6 +206,7 @@ struct HipEngine::Impl {
   bool ps_fp16 = false;         // config 5: fp16 power spectrum between pass 3 and the harmonic sum
   // harmonic-sum variant: harmonics 1..n staged in LDS, the rest gathered (BRP_HS_STAGE)
   int hs_stage = 0;
+  uint32_t hs_tile = 0;         // harmonic-sum bins per workgroup (wisdom / BRP_HS_TILE, 0 = kHsTile)
   uint32_t persist_per_cu = 4;  // persistent FFT passes: workgroups per CU (BRP_PERSIST, 0 = off)
   uint32_t ps_stride = 0;
   uint32_t i_start = 0;
@@ -443,6 +444,7 @@ struct HipEngine::Impl {
         ah.list = cands.p;
         ah.cap = cap;
         ah.staged_harmonics = hs_stage;
+        ah.tile = hs_tile;
         return hipk::launch_harmonic_sum(ah, nb, stream);
       }
       case kEpilogue:
@@ -573,12 +575,17 @@ int HipEngine::setup(const SearchGeometry& g, const std::vector<float>& series, 
   // measured settings for this (arch, M) from the plan wisdom; environment wins
   const PlanWisdom wis = load_wisdom(wisdom_path(), d.arch, d.plan.M);
   if (wis.found)
-    log_message(LOG_DEBUG, true, "Plan wisdom for %s M=%u: persist %d, FFT passes %d, HS stage %d\n", d.arch.c_str(),
-                d.plan.M, wis.persist_per_cu, wis.fft_passes, wis.hs_stage);
+    log_message(LOG_DEBUG, true, "Plan wisdom for %s M=%u: persist %d, FFT passes %d, HS stage %d, HS tile %d\n",
+                d.arch.c_str(), d.plan.M, wis.persist_per_cu, wis.fft_passes, wis.hs_stage, wis.hs_tile);
   if (wis.persist_per_cu >= 0) d.persist_per_cu = static_cast<uint32_t>(wis.persist_per_cu);
   if (const char* e = std::getenv("BRP_PERSIST")) d.persist_per_cu = static_cast<uint32_t>(std::atoi(e));
   d.hs_stage = wis.hs_stage >= 0 ? wis.hs_stage : 0;
   if (const char* e = std::getenv("BRP_HS_STAGE")) d.hs_stage = std::atoi(e);
+  // 1008 bins per workgroup: the tile plus its 4-bin halo fit in 4 x 256
+  // lanes (1024 leaves a fifth pass of 4 lanes), +1.4% templates/s
+  d.hs_tile = wis.hs_tile > 0 ? static_cast<uint32_t>(wis.hs_tile) : 1008u;
+  if (const char* e = std::getenv("BRP_HS_TILE")) d.hs_tile = static_cast<uint32_t>(std::atoi(e));
+  if (d.hs_stage != 0) d.hs_tile = hipk::kHsTile;  // the LDS staging layout is built for the default tile
   d.plan.persist_wgs = d.persist_per_cu * d.num_cus;
   // opt-in (BRP_FFT2=1): measured 84 vs 78 us/template sequential, the
   // three-pass kernels keep more workgroups per CU (profiles/README.md)

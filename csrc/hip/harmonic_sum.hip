@@ -85,18 +85,22 @@ __device__ __forceinline__ void stage_for_each(F&& f) {
 // are staged in LDS (their runs are short, l/16 bins per i, and shared by
 // many lanes of a gather), harmonics SMAX+1..16 are gathered per i from
 // global memory: SMAX = 0 gathers all, 16 stages all.
-template <typename T, int SMAX>
+template <typename T, int SMAX, int TILE>
 __global__ void __launch_bounds__(kThreads) harmonic_sum_kernel(HSArgs a) {
 #pragma clang fp contract(off)
   constexpr bool STAGED = SMAX > 0;
+  static_assert(!STAGED || TILE == kHsTile, "LDS staging is laid out for the default tile");
+  static_assert(TILE % 16 == 0, "tiles start at i == 8 mod 16");
+  constexpr int SPAN = TILE + kHalo;
+  constexpr int SPAN_PAD = SPAN + SPAN / 16 + 1;
   // staged segments, then (after a barrier) S_1..S_4 over the tile + halo
-  __shared__ __attribute__((aligned(16))) float lds[stage_lds_floats(SMAX)];
-  float (*sv)[kSpanPad] = reinterpret_cast<float (*)[kSpanPad]>(lds);
+  __shared__ __attribute__((aligned(16))) float lds[STAGED ? stage_lds_floats(SMAX) : 4 * SPAN_PAD];
+  float (*sv)[SPAN_PAD] = reinterpret_cast<float (*)[SPAN_PAD]>(lds);
   const int b = blockIdx.y;
   const T* P = reinterpret_cast<const T*>(sizeof(T) == 4 ? static_cast<const void*>(a.ps)
                                                         : static_cast<const void*>(a.ps16)) +
                static_cast<size_t>(b) * a.ps_stride;
-  const uint32_t i0 = a.i_start + blockIdx.x * kHsTile;
+  const uint32_t i0 = a.i_start + blockIdx.x * TILE;
   const float ninf = -__builtin_inff();
   auto lo4 = [&](uint32_t l) { return ((l * i0 + 8u) >> 4) & ~3u; };
 
@@ -141,7 +145,7 @@ __global__ void __launch_bounds__(kThreads) harmonic_sum_kernel(HSArgs a) {
     return static_cast<float>(P[bin]);
   };
 
-  constexpr int kIt = (kSpan + kThreads - 1) / kThreads;
+  constexpr int kIt = (SPAN + kThreads - 1) / kThreads;
   float s1[kIt], s2[kIt], s3[kIt], s4[kIt], p0[kIt];
 #pragma unroll
   for (int it = 0; it < kIt; ++it) {
@@ -149,7 +153,7 @@ __global__ void __launch_bounds__(kThreads) harmonic_sum_kernel(HSArgs a) {
     const uint32_t i = i0 + t;
     s1[it] = s2[it] = s3[it] = s4[it] = ninf;
     p0[it] = 0.0f;
-    if (t < kSpan && i >= a.w2 && i < a.hhi) {
+    if (t < SPAN && i >= a.w2 && i < a.hhi) {
       float sum = ld(16, i);
       p0[it] = sum;
       sum += ld(8, i);
@@ -166,7 +170,7 @@ __global__ void __launch_bounds__(kThreads) harmonic_sum_kernel(HSArgs a) {
 #pragma unroll
   for (int it = 0; it < kIt; ++it) {
     const int t = threadIdx.x + it * kThreads;
-    if (t < kSpan) {
+    if (t < SPAN) {
       sv[0][sidx(t)] = s1[it];
       sv[1][sidx(t)] = s2[it];
       sv[2][sidx(t)] = s3[it];
@@ -182,9 +186,9 @@ __global__ void __launch_bounds__(kThreads) harmonic_sum_kernel(HSArgs a) {
 #pragma unroll
   for (int it = 0; it < kIt; ++it) {
     const int t = threadIdx.x + it * kThreads;
-    if (t - static_cast<int>(threadIdx.x) >= kHsTile) break;  // uniform: whole iterations past the tile
+    if (t - static_cast<int>(threadIdx.x) >= TILE) break;  // uniform: whole iterations past the tile
     const uint32_t i = i0 + t;
-    const bool in = t < kHsTile && (i >= a.w2 && i < a.fhi);
+    const bool in = t < TILE && (i >= a.w2 && i < a.fhi);
     const float p = in ? p0[it] : 0.0f;
     emit(count, list, a.cap, in && p > thr0, hs_pack(b, 0, i), p);
   }
@@ -197,7 +201,7 @@ __global__ void __launch_bounds__(kThreads) harmonic_sum_kernel(HSArgs a) {
     const int off = g >> 1;
     const float thr = a.thr[static_cast<size_t>(b) * kHsThrStride + h];
     const int first = static_cast<int>((off - (i0 % g) + g) % g);
-    const int ngroups = (kHsTile - first + g - 1) / g;
+    const int ngroups = (TILE - first + g - 1) / g;
     for (int q = threadIdx.x; q < ((ngroups + kThreads - 1) / kThreads) * kThreads; q += kThreads) {
       bool pred = false;
       uint32_t j = 0;
@@ -219,23 +223,33 @@ __global__ void __launch_bounds__(kThreads) harmonic_sum_kernel(HSArgs a) {
 
 }  // namespace
 
-uint32_t hs_num_tiles(uint32_t i_start, uint32_t hhi) {
+uint32_t hs_num_tiles(uint32_t i_start, uint32_t hhi, uint32_t tile) {
   if (hhi <= i_start) return 0;
-  return (hhi - i_start + kHsTile - 1) / kHsTile;
+  return (hhi - i_start + tile - 1) / tile;
 }
 
 hipError_t launch_harmonic_sum(const HSArgs& a, int batch, hipStream_t s) {
-  const uint32_t tiles = hs_num_tiles(a.i_start, a.hhi);
+  const uint32_t tile = a.tile != 0 ? a.tile : kHsTile;
+  if (a.staged_harmonics != 0 && tile != kHsTile) return hipErrorInvalidValue;
+  const uint32_t tiles = hs_num_tiles(a.i_start, a.hhi, tile);
   if (tiles == 0) return hipSuccess;
   const dim3 grid(tiles, batch);
-#define BRP_HS_LAUNCH(SM)                                                                                   \
-  if (a.ps16 != nullptr) hipLaunchKernelGGL((harmonic_sum_kernel<_Float16, SM>), grid, dim3(kThreads), 0, s, a); \
-  else hipLaunchKernelGGL((harmonic_sum_kernel<float, SM>), grid, dim3(kThreads), 0, s, a);
+#define BRP_HS_LAUNCH(SM, TL)                                                                                   \
+  if (a.ps16 != nullptr) hipLaunchKernelGGL((harmonic_sum_kernel<_Float16, SM, TL>), grid, dim3(kThreads), 0, s, a); \
+  else hipLaunchKernelGGL((harmonic_sum_kernel<float, SM, TL>), grid, dim3(kThreads), 0, s, a);
   switch (a.staged_harmonics) {
-    case 0: BRP_HS_LAUNCH(0) break;
-    case 4: BRP_HS_LAUNCH(4) break;
-    case 8: BRP_HS_LAUNCH(8) break;
-    case 16: BRP_HS_LAUNCH(16) break;
+    case 0:
+      switch (tile) {
+        case kHsTile: BRP_HS_LAUNCH(0, kHsTile) break;
+        case 1008: BRP_HS_LAUNCH(0, 1008) break;
+        case 2032: BRP_HS_LAUNCH(0, 2032) break;
+        case 496: BRP_HS_LAUNCH(0, 496) break;
+        default: return hipErrorInvalidValue;
+      }
+      break;
+    case 4: BRP_HS_LAUNCH(4, kHsTile) break;
+    case 8: BRP_HS_LAUNCH(8, kHsTile) break;
+    case 16: BRP_HS_LAUNCH(16, kHsTile) break;
     default: return hipErrorInvalidValue;
   }
 #undef BRP_HS_LAUNCH

@@ -22,6 +22,7 @@ struct HSArgs {
   uint2* list;
   uint32_t cap;
   int staged_harmonics;   // harmonics 1..n staged in LDS (0, 4, 8 or 16), the rest gathered per i
+  uint32_t tile;          // bins i per workgroup (0 = kHsTile; 496, 1008, 2032 without staging)
 };
 
 constexpr uint32_t kHsThrStride = 8;  // floats per template in the threshold array (5 used)
@@ -31,7 +32,7 @@ __host__ __device__ constexpr uint32_t hs_pack(uint32_t k, uint32_t h, uint32_t 
   return (k << 26) | (h << kHsBinBits) | bin;
 }
 
-uint32_t hs_num_tiles(uint32_t i_start, uint32_t hhi);
+uint32_t hs_num_tiles(uint32_t i_start, uint32_t hhi, uint32_t tile = kHsTile);
 hipError_t launch_harmonic_sum(const HSArgs& a, int batch, hipStream_t s);
 
 }  // namespace hipk

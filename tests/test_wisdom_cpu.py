@@ -11,11 +11,11 @@ def test_wisdom_lookup(brp, tmp_path):
     p.write_text('{"entries": [\n'
                  '  {"arch": "gfx942", "M": 6291456, "persist_per_cu": 2, "fft_passes": 3, "hs_stage": 0},\n'
                  '  {"arch": "gfx950", "M": 6291456, "persist_per_cu": 6, "fft_passes": 2, "hs_stage": 8,'
-                 ' "batch": 1, "pipelines": 3, "date": "2026-10-16"},\n'
+                 ' "hs_tile": 1008, "batch": 1, "pipelines": 3, "date": "2026-10-16"},\n'
                  '  {"arch": "gfx950", "M": 2097152, "persist_per_cu": 8}\n]}\n')
     w = brp.load_wisdom(str(p), "gfx950:sramecc+:xnack-", 6291456)
     assert w["found"] and w["persist_per_cu"] == 6 and w["fft_passes"] == 2 and w["hs_stage"] == 8
-    assert w["batch"] == 1 and w["pipelines"] == 3
+    assert w["batch"] == 1 and w["pipelines"] == 3 and w["hs_tile"] == 1008
     w = brp.load_wisdom(str(p), "gfx950", 2097152)
     assert w["found"] and w["persist_per_cu"] == 8 and w["fft_passes"] == -1
     assert not brp.load_wisdom(str(p), "gfx950", 123)["found"]

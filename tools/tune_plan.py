@@ -97,10 +97,24 @@ def main() -> int:
         print(json.dumps(conc[-1]), flush=True)
     bc = max(conc, key=lambda r: r["templates_per_s"])
 
+    # stage 3: harmonic-sum tile at the chosen concurrency (no effect in isolation)
+    tiles = []
+    for tile in (1008, 1024, 496):
+        r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--steps", "2", "--warmup", "1", "--templates",
+                            str(args.templates), "--batch", str(bc["batch"]), "--streams", str(bc["pipelines"])],
+                           env=dict(env, BRP_HS_TILE=str(tile)), capture_output=True, text=True, timeout=600)
+        line = [l for l in r.stdout.splitlines() if l.startswith("{")]
+        if r.returncode != 0 or not line:
+            print(r.stderr[-2000:], file=sys.stderr)
+            return 1
+        tiles.append(dict(hs_tile=tile, templates_per_s=json.loads(line[-1])["value"]))
+        print(json.dumps(tiles[-1]), flush=True)
+    bt = max(tiles, key=lambda r: r["templates_per_s"])
+
     entry = dict(arch=arch, M=int(M), persist_per_cu=best["persist_per_cu"], fft_passes=best["fft_passes"],
-                 hs_stage=best["hs_stage"], batch=bc["batch"], pipelines=bc["pipelines"],
+                 hs_stage=best["hs_stage"], hs_tile=bt["hs_tile"], batch=bc["batch"], pipelines=bc["pipelines"],
                  us_per_template_sequential=best["us_per_template"], templates_per_s=bc["templates_per_s"],
-                 date=datetime.date.today().isoformat(), stage1=results, stage2=conc)
+                 date=datetime.date.today().isoformat(), stage1=results, stage2=conc, stage3=tiles)
     out = Path(args.out)
     doc = {"entries": []}
     if out.exists():
@@ -110,7 +124,7 @@ def main() -> int:
     out.parent.mkdir(parents=True, exist_ok=True)
     # one flat object per entry line (the C++ reader scans flat objects):
     # the per-candidate measurements go to a sibling file
-    flat = [{k: v for k, v in e.items() if k not in ("stage1", "stage2")} for e in doc["entries"]]
+    flat = [{k: v for k, v in e.items() if k not in ("stage1", "stage2", "stage3")} for e in doc["entries"]]
     out.write_text("{\"entries\": [\n" + ",\n".join("  " + json.dumps(e) for e in flat) + "\n]}\n")
     out.with_suffix(".measurements.json").write_text(json.dumps(doc, indent=1) + "\n")
     print(f"wrote {out}: {json.dumps(flat[-1])}")
