@@ -243,7 +243,13 @@ int SearchSession::prepare() {
   trace::Range range("brp:prepare");
   d.series = d.wu.samples;
   boinc::begin_critical_section();
-  int rc = d.backends[0]->setup(d.g, d.opt, d.series, d.zaps);
+  // the host copy of the whitened series only feeds backends that cannot take
+  // it device to device
+  bool adopt_all = true;
+  for (size_t k = 1; k < d.backends.size(); ++k) adopt_all = adopt_all && d.backends[k]->can_setup_from(*d.backends[0], d.g);
+  SearchOptions opt0 = d.opt;
+  opt0.device_series = adopt_all;
+  int rc = d.backends[0]->setup(d.g, opt0, d.series, d.zaps);
   if (rc) {
     boinc::end_critical_section();
     return rc;
@@ -255,6 +261,9 @@ int SearchSession::prepare() {
   // concurrent setups from several host threads measured no faster: the HIP
   // runtime serialises the allocations and uploads)
   for (size_t k = 1; k < d.backends.size(); ++k) {
+    // same device, same shape as last pass: device-to-device copy of the
+    // first backend's whitened series (no host round trip)
+    if (d.backends[k]->setup_from(*d.backends[0], d.g) == 0) continue;
     std::vector<float> s = d.series;
     rc = d.backends[k]->setup(d.g, opt_nw, s, d.zaps);
     if (rc) {

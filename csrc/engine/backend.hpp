@@ -43,6 +43,18 @@ class Backend {
   // thresholds of every template in the batch).
   virtual int process(const TemplateInput* t, int n, const float thr[kNumHarmonicLevels],
                       std::vector<TemplateCands>& out) = 0;
+  // Same-device shortcut for the next pass: take `first`'s prepared (whitened)
+  // series without a host round trip. Nonzero: not applicable, use setup().
+  virtual bool can_setup_from(const Backend& first, const SearchGeometry& g) const {
+    (void)first;
+    (void)g;
+    return false;
+  }
+  virtual int setup_from(const Backend& first, const SearchGeometry& g) {
+    (void)first;
+    (void)g;
+    return -1;
+  }
   virtual int preferred_batch() const = 0;
   virtual BackendStats stats() const { return {}; }
 };

@@ -674,6 +674,21 @@ int HipEngine::setup(const SearchGeometry& g, const std::vector<float>& series, 
 
 int HipEngine::upload_series(const std::vector<float>& series, float mu0) { return load_slot(0, series, mu0); }
 
+int HipEngine::adopt_series(const HipEngine& src) {
+  Impl& d = *impl_;
+  const Impl& s = *src.impl_;
+  if (!d.ready || !s.ready || d.device != s.device || d.slots != 1 || s.slots != 1 || !same_geometry(d.g, s.g))
+    return RADPUL_EVAL;
+  trace::Range range("brp:adopt_series");
+  BRP_HIP_CHECK(hipSetDevice(d.device), RADPUL_HIP_DEVICE_SET);
+  d.g = s.g;
+  d.mu0s = s.mu0s;
+  BRP_HIP_CHECK(hipMemcpyAsync(d.series.p, s.series.p, d.g.n_unpadded * sizeof(float), hipMemcpyDeviceToDevice, s.stream),
+                RADPUL_HIP_MEM_COPY_HOST_DEVICE);
+  BRP_HIP_CHECK(hipStreamSynchronize(s.stream), RADPUL_HIP_MEM_COPY_HOST_DEVICE);
+  return 0;
+}
+
 int HipEngine::set_slots(uint32_t k) {
   Impl& d = *impl_;
   if (k == 0 || k > (1u << 16)) return RADPUL_EVAL;
@@ -685,6 +700,8 @@ int HipEngine::set_slots(uint32_t k) {
 }
 
 uint32_t HipEngine::slots() const { return impl_->slots; }
+
+bool HipEngine::ps_fp16() const { return impl_->ps_fp16; }
 
 void HipEngine::set_ps_fp16(bool on) {
   Impl& d = *impl_;
@@ -705,8 +722,12 @@ int HipEngine::load_slot(uint32_t k, const std::vector<float>& series, float mu0
   return 0;
 }
 
+bool HipEngine::prepared_for(const SearchGeometry& g) const {
+  return impl_->ready && impl_->slots == 1 && same_geometry(impl_->g, g);
+}
+
 int HipEngine::whiten(const SearchOptions& opt, const std::vector<ZapRange>& zaps, std::vector<float>& series,
-                      uint32_t slot) {
+                      uint32_t slot, bool copy_back) {
   Impl& d = *impl_;
   if (slot >= d.slots) return RADPUL_EVAL;
   float* slot_series = d.series.p + static_cast<size_t>(slot) * d.g.n_unpadded;
@@ -831,8 +852,9 @@ int HipEngine::whiten(const SearchOptions& opt, const std::vector<ZapRange>& zap
   ap.real_out = slot_series;
   ap.n_out = g.n_unpadded;
   BRP_HIP_CHECK(hipk::launch_pass3_plain(d.plan, ap, s), RADPUL_HIP_KERNEL_INVOKE);
-  BRP_HIP_CHECK(hipMemcpyAsync(series.data(), slot_series, g.n_unpadded * sizeof(float), hipMemcpyDeviceToHost, s),
-                RADPUL_HIP_MEM_COPY_DEVICE_HOST);
+  if (copy_back)
+    BRP_HIP_CHECK(hipMemcpyAsync(series.data(), slot_series, g.n_unpadded * sizeof(float), hipMemcpyDeviceToHost, s),
+                  RADPUL_HIP_MEM_COPY_DEVICE_HOST);
   BRP_HIP_CHECK(hipStreamSynchronize(s), RADPUL_HIP_KERNEL_INVOKE);
   d.mu0s[slot] = 0.0f;  // whitened series has its DC (and first window_2 bins) removed
   d.st.whiten_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -1128,12 +1150,21 @@ class HipBackend final : public Backend {
     eng_.set_ps_fp16(opt.ps_fp16);
     int rc = eng_.setup(g, series, static_cast<float>(mean));
     if (rc) return rc;
-    if (opt.white) return eng_.whiten(opt, zaps, series);
+    if (opt.white) return eng_.whiten(opt, zaps, series, 0, !opt.device_series);
     return 0;
   }
   int process(const TemplateInput* t, int n, const float thr[kNumHarmonicLevels],
               std::vector<TemplateCands>& out) override {
     return eng_.process(t, n, thr, out);
+  }
+  bool can_setup_from(const Backend& first, const SearchGeometry& g) const override {
+    const auto* src = dynamic_cast<const HipBackend*>(&first);
+    return src != nullptr && src != this && eng_.ps_fp16() == src->eng_.ps_fp16() && eng_.device() == src->eng_.device() &&
+           eng_.prepared_for(g) && src->eng_.prepared_for(g);
+  }
+  int setup_from(const Backend& first, const SearchGeometry& g) override {
+    if (!can_setup_from(first, g)) return -1;
+    return eng_.adopt_series(dynamic_cast<const HipBackend&>(first).eng_) == 0 ? 0 : -1;
   }
   int preferred_batch() const override { return eng_.batch(); }
   BackendStats stats() const override { return eng_.stats(); }

@@ -22,6 +22,10 @@ class HipEngine {
   // subtracted before the FFT (keeps the padding correction well conditioned)
   int setup(const SearchGeometry& g, const std::vector<float>& series, float mu0);
   int upload_series(const std::vector<float>& series, float mu0);
+  // Re-setup for the next pass over the same geometry by a device-to-device
+  // copy of `src`'s (whitened) series: `src` and this engine share a device and
+  // this engine was set up before. Returns RADPUL_EVAL when not applicable.
+  int adopt_series(const HipEngine& src);
   // Multi-WU batching: the series buffer holds `k` work units of the same
   // shape (set before setup(); setup() fills slot 0, load_slot() the others).
   // Templates pick their slot with TemplateInput::wu.
@@ -29,12 +33,15 @@ class HipEngine {
   // config 5: store the power spectrum as fp16 (halves the pass-3 write and the
   // harmonic-sum reads; the sums stay fp32 in the reference order)
   void set_ps_fp16(bool on);
+  bool ps_fp16() const;
   uint32_t slots() const;
   int load_slot(uint32_t k, const std::vector<float>& series, float mu0);
   // whitening + zapping of one slot on the device; `series` (that slot's raw
   // data) receives the whitened data
   int whiten(const SearchOptions& opt, const std::vector<ZapRange>& zaps, std::vector<float>& series,
-             uint32_t slot = 0);
+             uint32_t slot = 0, bool copy_back = true);
+  // set up (buffers, plan, graphs) for this geometry with one WU slot
+  bool prepared_for(const SearchGeometry& g) const;
   int process(const TemplateInput* t, int n, const float thr[kNumHarmonicLevels], std::vector<TemplateCands>& out);
   // per-template thresholds thr[i * thr_stride + h] (thr_stride 0: shared)
   int process(const TemplateInput* t, int n, const float* thr, int thr_stride, std::vector<TemplateCands>& out);
