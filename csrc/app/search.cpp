@@ -143,6 +143,7 @@ struct SearchSession::Impl {
   std::vector<TemplateInput> tin;
   std::vector<std::unique_ptr<Backend>> backends;
   std::vector<float> series;  // whitened (or raw) series used for templates
+  std::shared_ptr<void> wu_pin;  // wu.samples page-locked for the per-pass upload (released first)
 };
 
 SearchSession::SearchSession() : impl_(new Impl) {}
@@ -241,7 +242,6 @@ int SearchSession::open(const SearchOptions& opt, const SearchControl& ctl) {
 int SearchSession::prepare() {
   Impl& d = *impl_;
   trace::Range range("brp:prepare");
-  d.series = d.wu.samples;
   boinc::begin_critical_section();
   // the host copy of the whitened series only feeds backends that cannot take
   // it device to device
@@ -249,7 +249,13 @@ int SearchSession::prepare() {
   for (size_t k = 1; k < d.backends.size(); ++k) adopt_all = adopt_all && d.backends[k]->can_setup_from(*d.backends[0], d.g);
   SearchOptions opt0 = d.opt;
   opt0.device_series = adopt_all;
-  int rc = d.backends[0]->setup(d.g, opt0, d.series, d.zaps);
+  const bool hip0 = std::strcmp(d.backends[0]->name(), "hip") == 0;
+  if (hip0 && !d.wu_pin) d.wu_pin = hip_pin_host(d.wu.samples.data(), d.wu.samples.size() * sizeof(float));
+  // a HIP backend that keeps the whitened series on the device only reads
+  // the raw samples: upload them straight from the (page-locked) WU buffer
+  const bool direct = hip0 && adopt_all;
+  if (!direct) d.series = d.wu.samples;
+  int rc = d.backends[0]->setup(d.g, opt0, direct ? d.wu.samples : d.series, d.zaps);
   if (rc) {
     boinc::end_critical_section();
     return rc;

@@ -68,5 +68,8 @@ std::unique_ptr<Backend> make_hip_backend(int device, int batch, int* err);
 // Host waits on HIP work sleep (hipDeviceScheduleBlockingSync) instead of
 // spinning; set before the first backend is created (the BOINC app does).
 void hip_set_blocking_sync(bool on);
+// Page-lock an existing host range for direct DMA (hipHostRegister) for the
+// lifetime of the returned handle; empty handle if the runtime refuses.
+std::shared_ptr<void> hip_pin_host(void* p, size_t bytes);
 
 }  // namespace brp

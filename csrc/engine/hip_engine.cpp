@@ -1174,6 +1174,14 @@ class HipBackend final : public Backend {
 };
 }  // namespace
 
+std::shared_ptr<void> hip_pin_host(void* p, size_t bytes) {
+  if (p == nullptr || bytes == 0 || hipHostRegister(p, bytes, hipHostRegisterDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    return {};
+  }
+  return std::shared_ptr<void>(p, [](void* q) { (void)hipHostUnregister(q); });
+}
+
 bool hip_backend_supports(const SearchGeometry& g) {
   FFTPlan3 p;
   return g.nsamples % 2 == 0 && make_fft_plan(g.nsamples / 2, p);
