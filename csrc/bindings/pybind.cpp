@@ -270,6 +270,15 @@ PYBIND11_MODULE(_brp, m) {
       .def("get", &Taus2::get)
       .def("uniform", &Taus2::uniform);
   m.def("gaussian_ziggurat", &gaussian_ziggurat);
+  m.def("hip_running_median", [](py::array_t<float, py::array::c_style> x, uint32_t w, int reps, int device) {
+    std::vector<float> in(x.data(), x.data() + x.size()), out;
+    double ms = 0;
+    {
+      py::gil_scoped_release rel;
+      check(hip_running_median(device, in, w, out, reps, &ms), "hip_running_median");
+    }
+    return py::make_tuple(py::array_t<float>(out.size(), out.data()), ms);
+  }, py::arg("x"), py::arg("w"), py::arg("reps") = 0, py::arg("device") = 0);
   m.def("running_median", [](py::array_t<float, py::array::c_style> x, size_t w) {
     if (static_cast<size_t>(x.size()) < w || w == 0) throw std::invalid_argument("window larger than input");
     py::array_t<float> out(x.size() - w + 1);

@@ -71,5 +71,9 @@ void hip_set_blocking_sync(bool on);
 // Page-lock an existing host range for direct DMA (hipHostRegister) for the
 // lifetime of the returned handle; empty handle if the runtime refuses.
 std::shared_ptr<void> hip_pin_host(void* p, size_t bytes);
+// Device running median (whitening kernel) for tests and timing: out has
+// in.size() - W + 1 entries; `reps` timed launches after one warm-up.
+int hip_running_median(int device, const std::vector<float>& in, uint32_t W, std::vector<float>& out, int reps,
+                       double* ms_per_call);
 
 }  // namespace brp

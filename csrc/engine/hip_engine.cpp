@@ -502,6 +502,38 @@ void log_mem_status(int device, const char* when) {
 
 void hip_set_blocking_sync(bool on) { g_blocking_sync = on; }
 
+int hip_running_median(int device, const std::vector<float>& in, uint32_t W, std::vector<float>& out, int reps,
+                       double* ms_per_call) {
+  if (W == 0 || in.size() < W || !hipk::running_median_supported(W)) return RADPUL_EVAL;
+  BRP_HIP_CHECK(hipSetDevice(device < 0 ? 0 : device), RADPUL_HIP_DEVICE_SET);
+  DevBuf<float> din, dout;
+  int rc;
+  const size_t n_out = in.size() - W + 1;
+  if ((rc = din.alloc(in.size())) || (rc = dout.alloc(n_out))) return rc;
+  BRP_HIP_CHECK(hipMemcpy(din.p, in.data(), in.size() * sizeof(float), hipMemcpyHostToDevice),
+                RADPUL_HIP_MEM_COPY_HOST_DEVICE);
+  hipEvent_t e0, e1;
+  BRP_HIP_CHECK(hipEventCreate(&e0), RADPUL_HIP_DEVICE_SET);
+  BRP_HIP_CHECK(hipEventCreate(&e1), RADPUL_HIP_DEVICE_SET);
+  BRP_HIP_CHECK(hipk::launch_running_median(din.p, static_cast<uint32_t>(in.size()), W, dout.p, nullptr),
+                RADPUL_HIP_KERNEL_INVOKE);
+  BRP_HIP_CHECK(hipEventRecord(e0, nullptr), RADPUL_HIP_KERNEL_INVOKE);
+  for (int r = 0; r < reps; ++r)
+    BRP_HIP_CHECK(hipk::launch_running_median(din.p, static_cast<uint32_t>(in.size()), W, dout.p, nullptr),
+                  RADPUL_HIP_KERNEL_INVOKE);
+  BRP_HIP_CHECK(hipEventRecord(e1, nullptr), RADPUL_HIP_KERNEL_INVOKE);
+  BRP_HIP_CHECK(hipEventSynchronize(e1), RADPUL_HIP_KERNEL_INVOKE);
+  float ms = 0;
+  (void)hipEventElapsedTime(&ms, e0, e1);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  if (ms_per_call) *ms_per_call = reps > 0 ? ms / reps : 0.0;
+  out.resize(n_out);
+  BRP_HIP_CHECK(hipMemcpy(out.data(), dout.p, n_out * sizeof(float), hipMemcpyDeviceToHost),
+                RADPUL_HIP_MEM_COPY_DEVICE_HOST);
+  return 0;
+}
+
 int HipEngine::init(int device, int batch) {
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {

@@ -1,6 +1,8 @@
 // Whitening + RFI zapping kernels (reference demod_binary.c:857-1079, done on the
 // host with FFTW/rngmed/GSL there; on MI355X it runs on the device between a
 // forward and an inverse pass of the same hand-written FFT).
+#include <cstdlib>
+
 #include "hip_common.hpp"
 #include "whiten_kernels.hpp"
 
@@ -27,11 +29,16 @@ __global__ void whiten_power_kernel(const float2* spec, uint32_t n, float* ps) {
 // outputs: it finds the middle member of its first window by one scan of the
 // sorted span, then slides the window one sample at a time, moving the median
 // pointer past the removed / inserted ranks (O(1) members per step).
-template <int SPAN, int NT>
+//
+// CHUNKED: the first-window scan reads 8 sorted positions per 16-byte LDS
+// load (the same address for every lane: a broadcast) and counts members
+// branch-free, leaving the loop once every lane of the wave has found its
+// median; the plain scan waits on one dependent 2-byte LDS load per entry.
+template <int SPAN, int NT, bool CHUNKED>
 __global__ void __launch_bounds__(NT) running_median_kernel(const float* in, uint32_t n_in, uint32_t W, float* med,
                                                             uint32_t n_out, uint32_t per_block) {
   __shared__ float key[SPAN];
-  __shared__ uint16_t pos[SPAN];
+  __shared__ __attribute__((aligned(16))) uint16_t pos[SPAN];
   __shared__ uint16_t rank[SPAN];
   static_assert(SPAN <= 65536, "16-bit positions");
   const uint32_t o0 = blockIdx.x * per_block;
@@ -77,10 +84,31 @@ __global__ void __launch_bounds__(NT) running_median_kernel(const float* in, uin
   // first window: scan to the mid-th member
   int m = 0;
   uint32_t below = 0;  // members with sorted index < m
-  for (;; ++m) {
-    if (member(m, t0)) {
-      if (below == mid) break;
-      ++below;
+  if constexpr (CHUNKED) {
+    // lanes past their run (t0 >= t1) returned above; the rest scan together
+    const uint4* pos8 = reinterpret_cast<const uint4*>(pos);
+    int found = -1;
+    uint32_t cnt = 0;
+    for (int c = 0; c < SPAN / 8; ++c) {
+      const uint4 v = pos8[c];
+      const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint32_t p = (w4[k >> 1] >> (16 * (k & 1))) & 0xffffu;
+        const bool mem = (p - t0) < W;  // unsigned: t0 <= p < t0 + W
+        if (found < 0 && mem && cnt == mid) found = c * 8 + k;
+        cnt += mem ? 1u : 0u;
+      }
+      if (__all(found >= 0)) break;
+    }
+    m = found;
+    below = mid;
+  } else {
+    for (;; ++m) {
+      if (member(m, t0)) {
+        if (below == mid) break;
+        ++below;
+      }
     }
   }
   for (uint32_t t = t0;; ++t) {
@@ -164,8 +192,13 @@ hipError_t launch_running_median(const float* in, uint32_t n_in, uint32_t W, flo
   const uint32_t n_out = n_in - W + 1;
   constexpr int kSpan = 4096, kThreads = 256;
   const uint32_t per = kSpan - W + 1;
-  hipLaunchKernelGGL((running_median_kernel<kSpan, kThreads>), dim3((n_out + per - 1) / per), dim3(kThreads), 0, s, in,
-                     n_in, W, med, n_out, per);
+  static const bool plain = std::getenv("BRP_RMED_PLAIN") != nullptr;  // A/B switch
+  if (plain)
+    hipLaunchKernelGGL((running_median_kernel<kSpan, kThreads, false>), dim3((n_out + per - 1) / per), dim3(kThreads), 0,
+                       s, in, n_in, W, med, n_out, per);
+  else
+    hipLaunchKernelGGL((running_median_kernel<kSpan, kThreads, true>), dim3((n_out + per - 1) / per), dim3(kThreads), 0,
+                       s, in, n_in, W, med, n_out, per);
   return hipGetLastError();
 }
 

@@ -148,3 +148,15 @@ def test_two_pass_fft_matches_cpu(brp, gpu, monkeypatch):
         err = np.abs(ps_gpu[1:lim].astype(np.float64) - ps_cpu[1:lim]) / np.maximum(ps_cpu[1:lim], scale)
         assert np.percentile(err, 99.9) < 2e-5, (k, np.percentile(err, 99.9))
         assert err.max() < 1e-3, (k, err.max(), int(np.argmax(err)) + 1)
+
+
+@pytest.mark.parametrize("w", [1, 2, 99, 100, 1000, 3072])
+def test_running_median_kernel_bit_exact(brp, gpu, w):
+    """Device running median == host Mohanty running median, bit for bit, with ties."""
+    rng = np.random.default_rng(w)
+    x = rng.exponential(size=50_000 + 3 * w).astype(np.float32)
+    x[::7] = np.round(x[::7], 1)  # many exact ties
+    ref = brp.running_median(x, w)
+    got, _ = brp.hip_running_median(x, w)
+    assert got.shape == ref.shape
+    assert np.array_equal(got, ref)
