@@ -231,6 +231,8 @@ struct HipEngine::Impl {
   DevBuf<float2> tw_hi, tw_lo;
   DevBuf<float2> w_spec, w_z;   // whitening scratch: half spectrum, packed inverse input
   DevBuf<float> w_psw, w_med;   // whitening scratch: power spectrum, running median
+  DevBuf<uint32_t> w_zbins;     // whitening: zapped bins and their noise
+  DevBuf<float2> w_znoise;
   DevBuf<float2> t_st1, t_st2, t_st3, t_p1, t_p2col, t_p2lo, t_p2hi, t_p3;
   DevBuf<float2> t_w768, t_t256, t_t4096, t_t8192;  // two-pass tables
   DevBuf<float> pss;            // [batch][M] slab-major power spectrum (two-pass)
@@ -589,6 +591,7 @@ int HipEngine::setup(const SearchGeometry& g, const std::vector<float>& series, 
     d.g = g;
     d.mu0s.assign(d.slots, 0.0f);
     d.mu0s[0] = mu0;
+    trace::Range up("brp:series_upload");
     BRP_HIP_CHECK(hipMemcpy(d.series.p, series.data(), g.n_unpadded * sizeof(float), hipMemcpyHostToDevice),
                   RADPUL_HIP_MEM_COPY_HOST_DEVICE);
     return 0;
@@ -761,6 +764,7 @@ bool HipEngine::prepared_for(const SearchGeometry& g) const {
 int HipEngine::whiten(const SearchOptions& opt, const std::vector<ZapRange>& zaps, std::vector<float>& series,
                       uint32_t slot, bool copy_back) {
   Impl& d = *impl_;
+  trace::Range range("brp:whiten");
   if (slot >= d.slots) return RADPUL_EVAL;
   float* slot_series = d.series.p + static_cast<size_t>(slot) * d.g.n_unpadded;
   const SearchGeometry& g = d.g;
@@ -829,9 +833,10 @@ int HipEngine::whiten(const SearchOptions& opt, const std::vector<ZapRange>& zap
   BRP_HIP_CHECK(hipk::launch_whiten_scale(spec.p, med.p, white_size, g.window_2, s), RADPUL_HIP_KERNEL_INVOKE);
   // RFI zapping: noise drawn on the host in the reference order (GSL-compatible RNG)
   ZapNoise noise;
+  trace::range_push("brp:zap_noise");
   make_zap_noise(seed, g, opt, zaps, noise);
-  DevBuf<uint32_t> zbins;
-  DevBuf<float2> znoise;
+  DevBuf<uint32_t>& zbins = d.w_zbins;
+  DevBuf<float2>& znoise = d.w_znoise;
   const uint32_t nz = static_cast<uint32_t>(noise.bin.size());
   // host sources of the async copies must outlive them: kept until the final
   // stream synchronisation of this function
@@ -850,9 +855,11 @@ int HipEngine::whiten(const SearchOptions& opt, const std::vector<ZapRange>& zap
     }
   }
   const uint32_t nzu = static_cast<uint32_t>(zb.size());
+  trace::range_pop();
   if (nzu) {
-    if ((rc = zbins.alloc(nzu))) return rc;
-    if ((rc = znoise.alloc(nzu))) return rc;
+    // kept across passes (a hipFree per pass would synchronise the device)
+    if (zbins.n < nzu && (rc = zbins.alloc(nzu))) return rc;
+    if (znoise.n < nzu && (rc = znoise.alloc(nzu))) return rc;
     BRP_HIP_CHECK(hipMemcpyAsync(zbins.p, zb.data(), nzu * sizeof(uint32_t), hipMemcpyHostToDevice, s),
                   RADPUL_HIP_MEM_COPY_HOST_DEVICE);
     BRP_HIP_CHECK(hipMemcpyAsync(znoise.p, zn.data(), nzu * sizeof(float2), hipMemcpyHostToDevice, s),
@@ -887,7 +894,10 @@ int HipEngine::whiten(const SearchOptions& opt, const std::vector<ZapRange>& zap
   if (copy_back)
     BRP_HIP_CHECK(hipMemcpyAsync(series.data(), slot_series, g.n_unpadded * sizeof(float), hipMemcpyDeviceToHost, s),
                   RADPUL_HIP_MEM_COPY_DEVICE_HOST);
-  BRP_HIP_CHECK(hipStreamSynchronize(s), RADPUL_HIP_KERNEL_INVOKE);
+  {
+    trace::Range wait("brp:whiten_wait");
+    BRP_HIP_CHECK(hipStreamSynchronize(s), RADPUL_HIP_KERNEL_INVOKE);
+  }
   d.mu0s[slot] = 0.0f;  // whitened series has its DC (and first window_2 bins) removed
   d.st.whiten_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return 0;
@@ -1171,7 +1181,7 @@ class HipBackend final : public Backend {
     // padding by linearity); a whitened series has its DC removed: mu0 = 0, the
     // value the whitening backend itself uses, so all devices compute identical spectra
     double mean = 0.0;
-    if (!opt.prewhitened) {
+    if (!opt.prewhitened && !opt.white) {  // whitening resets mu0 to 0 (the sum is a 4M-long serial chain)
       for (float v : series) mean += v;
       mean = series.empty() ? 0.0 : mean / series.size();
     }
