@@ -918,48 +918,49 @@ int HipEngine::process(const TemplateInput* t, int n, const float* thr, int thr_
   const SearchGeometry& g = d.g;
   for (int off = 0; off < n; off += d.batch) {
     const int nb = std::min(d.batch, n - off);
-    trace::range_push("brp:batch_launch");
-    for (int k = 0; k < nb; ++k) {
-      TemplateDev td{};
-      td.p = make_resamp_params(g.nsamples, g.n_unpadded, g.fft_size, g.dt, g.step_inv, t[off + k].P,
-                                t[off + k].tau, t[off + k].Psi0);
-      td.n_steps = resamp_n_steps(td.p, kSinLut, kCosLut);
-      if (t[off + k].wu >= d.slots) return RADPUL_EVAL;
-      td.wu = t[off + k].wu;
-      td.mu0 = d.mu0s[td.wu];
-      d.h_tmpl.p[k] = td;
-      const float* th = thr + static_cast<size_t>(off + k) * thr_stride;
-      for (int h = 0; h < kNumHarmonicLevels; ++h) d.h_thr.p[k * hipk::kHsThrStride + h] = th[h];
-    }
-    hipGraphExec_t exec = nullptr;
-    auto it = d.graphs.find(nb);
-    const bool use_graph = std::getenv("BRP_NO_GRAPH") == nullptr;
-    if (use_graph) {
-      if (it == d.graphs.end()) {
-        hipGraph_t graph;
-        BRP_HIP_CHECK(hipStreamBeginCapture(d.stream, hipStreamCaptureModeThreadLocal), RADPUL_HIP_GRAPH);
-        hipError_t e = d.enqueue(nb);
-        hipError_t e2 = hipStreamEndCapture(d.stream, &graph);
-        if (e != hipSuccess || e2 != hipSuccess) {
-          log_message(LOG_ERROR, true, "Graph capture failed: %s / %s\n", hipGetErrorName(e), hipGetErrorName(e2));
-          return RADPUL_HIP_GRAPH;
-        }
-        BRP_HIP_CHECK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0), RADPUL_HIP_GRAPH);
-        (void)hipGraphDestroy(graph);
-        d.graphs[nb] = exec;
-      } else {
-        exec = it->second;
+    {
+      trace::Range launch("brp:batch_launch");
+      for (int k = 0; k < nb; ++k) {
+        TemplateDev td{};
+        td.p = make_resamp_params(g.nsamples, g.n_unpadded, g.fft_size, g.dt, g.step_inv, t[off + k].P,
+                                  t[off + k].tau, t[off + k].Psi0);
+        td.n_steps = resamp_n_steps(td.p, kSinLut, kCosLut);
+        if (t[off + k].wu >= d.slots) return RADPUL_EVAL;
+        td.wu = t[off + k].wu;
+        td.mu0 = d.mu0s[td.wu];
+        d.h_tmpl.p[k] = td;
+        const float* th = thr + static_cast<size_t>(off + k) * thr_stride;
+        for (int h = 0; h < kNumHarmonicLevels; ++h) d.h_thr.p[k * hipk::kHsThrStride + h] = th[h];
       }
+      hipGraphExec_t exec = nullptr;
+      auto it = d.graphs.find(nb);
+      static const bool use_graph = std::getenv("BRP_NO_GRAPH") == nullptr;
+      if (use_graph) {
+        if (it == d.graphs.end()) {
+          hipGraph_t graph;
+          BRP_HIP_CHECK(hipStreamBeginCapture(d.stream, hipStreamCaptureModeThreadLocal), RADPUL_HIP_GRAPH);
+          hipError_t e = d.enqueue(nb);
+          hipError_t e2 = hipStreamEndCapture(d.stream, &graph);
+          if (e != hipSuccess || e2 != hipSuccess) {
+            log_message(LOG_ERROR, true, "Graph capture failed: %s / %s\n", hipGetErrorName(e), hipGetErrorName(e2));
+            return RADPUL_HIP_GRAPH;
+          }
+          BRP_HIP_CHECK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0), RADPUL_HIP_GRAPH);
+          (void)hipGraphDestroy(graph);
+          d.graphs[nb] = exec;
+        } else {
+          exec = it->second;
+        }
+      }
+      if (d.fg_in) std::atomic_thread_fence(std::memory_order_seq_cst);  // BAR writes before the launch
+      BRP_HIP_CHECK(hipEventRecord(d.ev0, d.stream), RADPUL_HIP_KERNEL_INVOKE);
+      if (use_graph) {
+        BRP_HIP_CHECK(hipGraphLaunch(exec, d.stream), RADPUL_HIP_GRAPH);
+      } else {
+        BRP_HIP_CHECK(d.enqueue(nb), RADPUL_HIP_KERNEL_INVOKE);
+      }
+      BRP_HIP_CHECK(hipEventRecord(d.ev1, d.stream), RADPUL_HIP_KERNEL_INVOKE);
     }
-    if (d.fg_in) std::atomic_thread_fence(std::memory_order_seq_cst);  // BAR writes before the launch
-    BRP_HIP_CHECK(hipEventRecord(d.ev0, d.stream), RADPUL_HIP_KERNEL_INVOKE);
-    if (use_graph) {
-      BRP_HIP_CHECK(hipGraphLaunch(exec, d.stream), RADPUL_HIP_GRAPH);
-    } else {
-      BRP_HIP_CHECK(d.enqueue(nb), RADPUL_HIP_KERNEL_INVOKE);
-    }
-    BRP_HIP_CHECK(hipEventRecord(d.ev1, d.stream), RADPUL_HIP_KERNEL_INVOKE);
-    trace::range_pop();
     {
       trace::Range wait("brp:batch_wait");
       BRP_HIP_CHECK(hipStreamSynchronize(d.stream), RADPUL_HIP_KERNEL_INVOKE);
