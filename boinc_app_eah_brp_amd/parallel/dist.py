@@ -118,8 +118,12 @@ def allgather_tables(table, ctx: DistContext) -> list:
         ctx.stalled = True
         time.sleep(2 * collective_timeout_s() + 1)
     try:
-        work = dist.all_gather_into_tensor(out, mine, async_op=True)
-        work.wait(timeout=timedelta(seconds=collective_timeout_s()))
+        if ctx.backend == "nccl":
+            # RCCL: the process group's own timeout (watchdog) bounds the call
+            dist.all_gather_into_tensor(out, mine)
+        else:
+            work = dist.all_gather_into_tensor(out, mine, async_op=True)
+            work.wait(timeout=timedelta(seconds=collective_timeout_s()))
         host = out.cpu().numpy()
     except Exception as e:  # gloo/RCCL timeout, peer gone, communicator error
         raise CollectiveError(f"rank {ctx.rank}: table all-gather failed: {e}") from e

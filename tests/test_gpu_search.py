@@ -216,3 +216,37 @@ def test_fine_grained_parameter_and_result_buffers(brp, gpu, case, tmp_path):
             assert "large BAR 1" in r.stdout + r.stderr
         runs[fg] = (tmp_path / fg / "res.cand").read_bytes()
     assert runs["in"] == runs["0"] and runs["out"] == runs["0"] and runs["both"] == runs["0"]
+
+
+_RCCL_SCRIPT = r"""
+import os, sys, torch, torch.distributed as dist
+sys.path.insert(0, os.environ["REPO"])
+from boinc_app_eah_brp_amd import native
+from boinc_app_eah_brp_amd.parallel import dist as bd
+dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+class Forced(bd.DistContext):
+    distributed = property(lambda self: True)
+ctx = Forced(rank=0, world=1, local_rank=0, backend="nccl", device=torch.device("cuda", 0))
+t = native().CandidateTable()
+got = bd.allgather_tables(t, ctx)
+assert len(got) == 1 and bytes(got[0].to_bytes()) == bytes(t.to_bytes())
+assert bd.max_over_ranks(3.5, ctx) == 3.5
+bd.barrier(ctx)
+dist.destroy_process_group()
+print("RCCL_OK")
+"""
+
+
+def test_rccl_collectives_single_rank(gpu, tmp_path):
+    """The RCCL calls of the sharded search (uint8 all-gather of the tables,
+    float64 max all-reduce, barrier) on a one-rank process group."""
+    import socket
+    import sys
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+               REPO=str(Path(__file__).resolve().parent.parent))
+    r = subprocess.run([sys.executable, "-c", _RCCL_SCRIPT], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and "RCCL_OK" in r.stdout, r.stderr[-3000:]
