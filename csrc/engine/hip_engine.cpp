@@ -206,6 +206,7 @@ struct HipEngine::Impl {
   bool ps_fp16 = false;         // config 5: fp16 power spectrum between pass 3 and the harmonic sum
   // harmonic-sum variant: harmonics 1..n staged in LDS, the rest gathered (BRP_HS_STAGE)
   int hs_stage = 0;
+  uint32_t hs_xcd = 0;          // BRP_HS_XCD=1: XCD-contiguous harmonic-sum tiles
   uint32_t hs_tile = 0;         // harmonic-sum bins per workgroup (wisdom / BRP_HS_TILE, 0 = kHsTile)
   uint32_t persist_per_cu = 4;  // persistent FFT passes: workgroups per CU (BRP_PERSIST, 0 = off)
   uint32_t ps_stride = 0;
@@ -447,6 +448,7 @@ struct HipEngine::Impl {
         ah.cap = cap;
         ah.staged_harmonics = hs_stage;
         ah.tile = hs_tile;
+        ah.xcd = hs_xcd;
         return hipk::launch_harmonic_sum(ah, nb, stream);
       }
       case kEpilogue:
@@ -620,6 +622,7 @@ int HipEngine::setup(const SearchGeometry& g, const std::vector<float>& series, 
   // lanes (1024 leaves a fifth pass of 4 lanes), +1.4% templates/s
   d.hs_tile = wis.hs_tile > 0 ? static_cast<uint32_t>(wis.hs_tile) : 1008u;
   if (const char* e = std::getenv("BRP_HS_TILE")) d.hs_tile = static_cast<uint32_t>(std::atoi(e));
+  if (const char* e = std::getenv("BRP_HS_XCD")) d.hs_xcd = static_cast<uint32_t>(std::atoi(e));
   if (d.hs_stage != 0) d.hs_tile = hipk::kHsTile;  // the LDS staging layout is built for the default tile
   d.plan.persist_wgs = d.persist_per_cu * d.num_cus;
   // opt-in (BRP_FFT2=1): measured 84 vs 78 us/template sequential, the

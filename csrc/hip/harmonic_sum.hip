@@ -100,7 +100,8 @@ __global__ void __launch_bounds__(kThreads) harmonic_sum_kernel(HSArgs a) {
   const T* P = reinterpret_cast<const T*>(sizeof(T) == 4 ? static_cast<const void*>(a.ps)
                                                         : static_cast<const void*>(a.ps16)) +
                static_cast<size_t>(b) * a.ps_stride;
-  const uint32_t i0 = a.i_start + blockIdx.x * TILE;
+  const uint32_t tile_id = a.xcd != 0 ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+  const uint32_t i0 = a.i_start + tile_id * TILE;
   const float ninf = -__builtin_inff();
   auto lo4 = [&](uint32_t l) { return ((l * i0 + 8u) >> 4) & ~3u; };
 

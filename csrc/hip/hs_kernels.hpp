@@ -23,6 +23,7 @@ struct HSArgs {
   uint32_t cap;
   int staged_harmonics;   // harmonics 1..n staged in LDS (0, 4, 8 or 16), the rest gathered per i
   uint32_t tile;          // bins i per workgroup (0 = kHsTile; 496, 1008, 2032 without staging)
+  uint32_t xcd;           // nonzero: consecutive tiles on one XCD (shared harmonic lines stay in its L2)
 };
 
 constexpr uint32_t kHsThrStride = 8;  // floats per template in the threshold array (5 used)
