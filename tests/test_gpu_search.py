@@ -218,6 +218,23 @@ def test_fine_grained_parameter_and_result_buffers(brp, gpu, case, tmp_path):
     assert runs["in"] == runs["0"] and runs["out"] == runs["0"] and runs["both"] == runs["0"]
 
 
+def test_harmonic_sum_variants_same_result(brp, gpu, case, tmp_path):
+    """Every harmonic-sum kernel instantiation (tiles of 496 / 1008 / 1024 /
+    2032 bins, harmonics staged in LDS, XCD-contiguous tiles) writes the same
+    result file as the default."""
+    variants = {"default": {}, "t496": dict(BRP_HS_TILE="496"), "t1024": dict(BRP_HS_TILE="1024"),
+                "t2032": dict(BRP_HS_TILE="2032"), "s4": dict(BRP_HS_STAGE="4"), "s8": dict(BRP_HS_STAGE="8"),
+                "s16": dict(BRP_HS_STAGE="16"), "xcd": dict(BRP_HS_XCD="1")}
+    runs = {}
+    for name, env in variants.items():
+        r = _app_gpu(case, tmp_path / name, **env)
+        assert r.returncode == 0, (name, r.stderr[-3000:])
+        runs[name] = (tmp_path / name / "res.cand").read_bytes()
+    assert len(runs["default"]) > 0
+    for name, got in runs.items():
+        assert got == runs["default"], name
+
+
 _RCCL_SCRIPT = r"""
 import os, sys, torch, torch.distributed as dist
 sys.path.insert(0, os.environ["REPO"])
