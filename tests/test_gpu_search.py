@@ -267,3 +267,55 @@ def test_rccl_collectives_single_rank(gpu, tmp_path):
                REPO=str(Path(__file__).resolve().parent.parent))
     r = subprocess.run([sys.executable, "-c", _RCCL_SCRIPT], env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0 and "RCCL_OK" in r.stdout, r.stderr[-3000:]
+
+
+_SHARD_SCRIPT = r"""
+import os, sys
+sys.path.insert(0, os.environ["REPO"])
+import json, numpy as np, torch, torch.distributed as dist
+from boinc_app_eah_brp_amd.parallel import dist as bd
+opts = json.loads(os.environ["OPTS"])
+ctx = bd.init_distributed("gloo")
+ss = bd.ShardedSearch(opts, ctx, device=0, streams=2)
+table = ss.step()
+if ctx.rank == 0:
+    np.save(os.environ["OUT"], np.asarray(table.to_bytes(), np.uint8))
+bd.barrier(ctx)
+dist.destroy_process_group()
+print("SHARD_OK", ctx.rank, ss.begin, ss.end)
+"""
+
+
+def test_two_rank_sharded_gpu_search_equals_single(brp, gpu, case, tmp_path):
+    """The multi-rank bench path with HIP engines: two ranks (gloo; RCCL
+    refuses two ranks on one GPU) each search half the bank on the GPU, the
+    all-gathered merge equals a one-rank search byte for byte."""
+    import json
+    import socket
+    import sys
+
+    import numpy as np
+
+    from boinc_app_eah_brp_amd.parallel import dist as bd
+
+    opts = dict(inputfile=case["wu"], templatebank=case["bank"], zaplistfile=case["zap"], f0=400.0, padding=3.0,
+                fA=0.08, window=100, white=True, batch=2, outputfile=str(tmp_path / "x.cand"))
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    out = tmp_path / "merged.npy"
+    procs = []
+    for rank in range(2):
+        env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE="2",
+                   LOCAL_RANK="0", OPTS=json.dumps(opts), OUT=str(out),
+                   REPO=str(Path(__file__).resolve().parent.parent))
+        procs.append(subprocess.Popen([sys.executable, "-c", _SHARD_SCRIPT], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    for p in procs:
+        so, se = p.communicate(timeout=240)
+        assert p.returncode == 0 and "SHARD_OK" in so, se[-3000:]
+
+    single = bd.ShardedSearch(opts, bd.DistContext(rank=0, world=1, local_rank=0, backend="none"), device=0,
+                              streams=2).step()
+    assert bytes(np.load(out)) == bytes(np.asarray(single.to_bytes(), np.uint8))
+    assert sum(1 for e in single.entries() if e[5] > 0) > 0
