@@ -4,6 +4,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -169,14 +170,21 @@ int MultiSession::run(uint32_t begin, uint32_t end, std::vector<CandidateTable>&
   std::map<uint64_t, Batch> ready;
   std::atomic<uint64_t> next{0};
   std::atomic<bool> stop{false};
-  // deal order: blocks of B templates, WU by WU within a block. A batch then
-  // holds templates of one WU (they share the series in L2), and every WU
-  // still sees its templates in increasing order.
+  // deal order: blocks of TB templates (a multiple of B), WU by WU within a
+  // block. A batch then holds templates of one WU, and every WU still sees its
+  // templates in increasing order. Long blocks keep all pipelines on the same
+  // WU, so one 16 MB series (not K of them) competes with the pipelines' FFT
+  // buffers for the 256 MB Infinity Cache. BRP_MULTI_BLOCK = batches per block.
+  static const uint32_t block_batches = [] {
+    const char* e = std::getenv("BRP_MULTI_BLOCK");
+    return e ? std::max(1, std::atoi(e)) : 64;
+  }();
+  const uint32_t TB = static_cast<uint32_t>(B) * block_batches;
   std::vector<std::pair<uint32_t, uint32_t>> order;  // (template, WU)
   order.reserve(npairs);
-  for (uint32_t t0 = begin; t0 < end; t0 += static_cast<uint32_t>(B))
+  for (uint32_t t0 = begin; t0 < end; t0 += TB)
     for (uint32_t w = 0; w < K; ++w)
-      for (uint32_t t = t0; t < std::min<uint32_t>(t0 + B, end); ++t) order.emplace_back(t, w);
+      for (uint32_t t = t0; t < std::min<uint32_t>(t0 + TB, end); ++t) order.emplace_back(t, w);
   auto pair_input = [&](uint64_t q) {
     const uint32_t t = order[q].first;
     const uint32_t w = order[q].second;
