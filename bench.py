@@ -155,6 +155,8 @@ def main() -> int:
         from boinc_app_eah_brp_amd.models.multi import same_shape_synthetic_wus
 
         hdr, _, _ = brp.read_work_unit(str(wu))
+        if ctx.rank == 0:
+            print(f"[bench] preparing {n_wus - 1} synthetic WUs", file=sys.stderr, flush=True)
         extra = same_shape_synthetic_wus(Path(os.environ.get("TMPDIR", "/tmp")) / "brp_bench_wus", hdr, n_wus - 1)
         cfg = SearchConfig.benchmark(str(wu), str(bank), str(zap), batch=args.batch, ps_fp16=args.ps_fp16)
         search = MultiWUSearch([str(wu)] + extra, cfg, pipelines=args.streams, ctx=ctx)
@@ -168,14 +170,21 @@ def main() -> int:
     if use_gpu:
         torch.cuda.synchronize()
 
+    def progress(msg):
+        # long runs (config 4 at many WUs) stay visibly alive on stderr; stdout keeps the one JSON line
+        if ctx.rank == 0:
+            print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
     table = None
-    for _ in range(args.warmup):
+    for w in range(args.warmup):
+        progress(f"warmup step {w + 1}/{args.warmup}")
         table = search.step(limit)
     first = bytes(first_table(table).to_bytes()) if table is not None else None
     barrier(ctx)
     if use_gpu:
         torch.cuda.synchronize()
     search.timings.clear()
+    progress(f"timing {args.steps} step(s)")
     t0 = time.perf_counter()
     for _ in range(args.steps):
         table = search.step(limit)
