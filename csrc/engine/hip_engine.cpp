@@ -220,6 +220,17 @@ struct HipEngine::Impl {
   bool fg_in = false, fg_out = false;
 
   DevBuf<float> series;
+  // read-only series of a sibling pipeline on the same device (adopt_series):
+  // one copy for all pipelines keeps the Infinity-Cache footprint down
+  const float* shared_series = nullptr;
+  const float* series_in() const { return shared_series != nullptr ? shared_series : series.p; }
+  // back to the engine's own series (before anything writes it)
+  void own_series() {
+    if (shared_series == nullptr) return;
+    shared_series = nullptr;
+    for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second);  // captured series pointer changed
+    graphs.clear();
+  }
   DevBuf<float2> buf;           // [batch][M]
   DevBuf<float> ps;             // [batch][ps_stride]
   DevBuf<double> partials;      // [batch][wg1]
@@ -348,7 +359,7 @@ struct HipEngine::Impl {
           hipk::ColAArgs aa{};
           aa.out = buf.p;
           aa.M = plan.M;
-          aa.series = series.p;
+          aa.series = series_in();
           aa.n_unpadded = g.n_unpadded;
           aa.tmpl = tmpl.p;
           aa.partials = partials.p;
@@ -363,7 +374,7 @@ struct HipEngine::Impl {
         a1.L3 = plan.L3;
         a1.tw = tw;
         a1.tb = tables();
-        a1.series = series.p;
+        a1.series = series_in();
         a1.n_unpadded = g.n_unpadded;
         a1.tmpl = tmpl.p;
         a1.partials = partials.p;
@@ -587,6 +598,7 @@ int HipEngine::setup(const SearchGeometry& g, const std::vector<float>& series, 
   trace::Range range("brp:engine_setup");
   Impl& d = *impl_;
   BRP_HIP_CHECK(hipSetDevice(d.device), RADPUL_HIP_DEVICE_SET);
+  d.own_series();
   if (d.ready && same_geometry(d.g, g)) {
     // next work unit of the same shape (or the same WU again): buffers, tables
     // and captured graphs stay valid; only the series and its mean change
@@ -721,9 +733,17 @@ int HipEngine::adopt_series(const HipEngine& src) {
   BRP_HIP_CHECK(hipSetDevice(d.device), RADPUL_HIP_DEVICE_SET);
   d.g = s.g;
   d.mu0s = s.mu0s;
-  BRP_HIP_CHECK(hipMemcpyAsync(d.series.p, s.series.p, d.g.n_unpadded * sizeof(float), hipMemcpyDeviceToDevice, s.stream),
-                RADPUL_HIP_MEM_COPY_HOST_DEVICE);
+  static const bool share = std::getenv("BRP_SHARE_SERIES") == nullptr || std::atoi(std::getenv("BRP_SHARE_SERIES")) != 0;
   BRP_HIP_CHECK(hipStreamSynchronize(s.stream), RADPUL_HIP_MEM_COPY_HOST_DEVICE);
+  const float* want = share ? s.series_in() : nullptr;
+  if (want != d.shared_series) {
+    d.shared_series = want;
+    for (auto& kv : d.graphs) (void)hipGraphExecDestroy(kv.second);  // captured series pointer changed
+    d.graphs.clear();
+  }
+  if (!share)
+    BRP_HIP_CHECK(hipMemcpy(d.series.p, s.series.p, d.g.n_unpadded * sizeof(float), hipMemcpyDeviceToDevice),
+                  RADPUL_HIP_MEM_COPY_HOST_DEVICE);
   return 0;
 }
 
@@ -753,6 +773,7 @@ int HipEngine::load_slot(uint32_t k, const std::vector<float>& series, float mu0
   Impl& d = *impl_;
   if (!d.ready || k >= d.slots || series.size() < d.g.n_unpadded) return RADPUL_EVAL;
   BRP_HIP_CHECK(hipSetDevice(d.device), RADPUL_HIP_DEVICE_SET);
+  d.own_series();
   d.mu0s[k] = mu0;
   BRP_HIP_CHECK(hipMemcpy(d.series.p + static_cast<size_t>(k) * d.g.n_unpadded, series.data(),
                           d.g.n_unpadded * sizeof(float), hipMemcpyHostToDevice),
@@ -769,6 +790,7 @@ int HipEngine::whiten(const SearchOptions& opt, const std::vector<ZapRange>& zap
   Impl& d = *impl_;
   trace::Range range("brp:whiten");
   if (slot >= d.slots) return RADPUL_EVAL;
+  d.own_series();
   float* slot_series = d.series.p + static_cast<size_t>(slot) * d.g.n_unpadded;
   const SearchGeometry& g = d.g;
   auto t0 = std::chrono::steady_clock::now();
@@ -1032,7 +1054,7 @@ int HipEngine::power_spectrum(const TemplateInput& t, std::vector<float>& ps_out
     hipk::ColAArgs aa{};
     aa.out = d.buf.p;
     aa.M = d.plan.M;
-    aa.series = d.series.p;
+    aa.series = d.series_in();
     aa.n_unpadded = g.n_unpadded;
     aa.tmpl = d.tmpl.p;
     aa.partials = d.partials.p;
@@ -1077,7 +1099,7 @@ int HipEngine::power_spectrum(const TemplateInput& t, std::vector<float>& ps_out
   a1.L3 = d.plan.L3;
   a1.tw = tw;
   a1.tb = d.tables();
-  a1.series = d.series.p;
+  a1.series = d.series_in();
   a1.n_unpadded = g.n_unpadded;
   a1.tmpl = d.tmpl.p;
   a1.partials = d.partials.p;

@@ -22,9 +22,12 @@ class HipEngine {
   // subtracted before the FFT (keeps the padding correction well conditioned)
   int setup(const SearchGeometry& g, const std::vector<float>& series, float mu0);
   int upload_series(const std::vector<float>& series, float mu0);
-  // Re-setup for the next pass over the same geometry by a device-to-device
-  // copy of `src`'s (whitened) series: `src` and this engine share a device and
-  // this engine was set up before. Returns RADPUL_EVAL when not applicable.
+  // Re-setup for the next pass over the same geometry from `src`'s (whitened)
+  // series: `src` and this engine share a device and this engine was set up
+  // before. The pipeline reads `src`'s series in place (one copy in the
+  // Infinity Cache for all pipelines; `src` must outlive the search pass), or
+  // copies it device to device with BRP_SHARE_SERIES=0. setup(), load_slot()
+  // and whiten() return to the engine's own buffer. RADPUL_EVAL when not applicable.
   int adopt_series(const HipEngine& src);
   // Multi-WU batching: the series buffer holds `k` work units of the same
   // shape (set before setup(); setup() fills slot 0, load_slot() the others).
