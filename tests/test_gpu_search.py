@@ -319,3 +319,18 @@ def test_two_rank_sharded_gpu_search_equals_single(brp, gpu, case, tmp_path):
                               streams=2).step()
     assert bytes(np.load(out)) == bytes(np.asarray(single.to_bytes(), np.uint8))
     assert sum(1 for e in single.entries() if e[5] > 0) > 0
+
+
+def test_pipelines_sharing_one_series_equal_single_pipeline(brp, gpu, case, tmp_path):
+    """Three pipelines on one device: after the first pass, pipelines 2 and 3
+    read pipeline 1's whitened series in place (HipEngine::adopt_series). Every
+    pass, the shared one included, gives the one-pipeline table byte for byte."""
+    from boinc_app_eah_brp_amd.parallel import dist as bd
+
+    opts = dict(inputfile=case["wu"], templatebank=case["bank"], zaplistfile=case["zap"], f0=400.0, padding=3.0,
+                fA=0.08, window=100, white=True, batch=1, outputfile=str(tmp_path / "x.cand"))
+    ctx = bd.DistContext(rank=0, world=1, local_rank=0, backend="none")
+    one = bytes(bd.ShardedSearch(opts, ctx, device=0, streams=1).step().to_bytes())
+    three = bd.ShardedSearch(opts, ctx, device=0, streams=3)
+    for _ in range(3):
+        assert bytes(three.step().to_bytes()) == one
