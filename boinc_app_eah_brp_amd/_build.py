@@ -31,7 +31,7 @@ ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0]
 HOST_SRCS = [
     "core/log.cpp", "core/io.cpp", "core/stats.cpp", "core/gsl_compat.cpp", "core/rngmed.cpp",
     "core/search_core.cpp", "core/cpu_fft.cpp", "core/cpu_backend.cpp", "core/wisdom.cpp", "core/trace.cpp",
-    "boinc/boinc_shim.cpp", "boinc/ipc.cpp",
+    "boinc/runtime.cpp", "boinc/crash.cpp", "boinc/ipc.cpp",
     "engine/cpu_engine.cpp", "engine/hip_engine.cpp",
     "app/search.cpp", "app/multi.cpp", "app/cli.cpp",
 ]

@@ -9,7 +9,7 @@
 #include <string>
 #include <vector>
 
-#include "../boinc/boinc_shim.hpp"
+#include "../boinc/runtime.hpp"
 #include "../boinc/ipc.hpp"
 #include "../core/errors.hpp"
 #include "../core/log.hpp"
@@ -221,7 +221,9 @@ int search_main(int argc, char** argv) {
     log_message(LOG_INFO, true, "Throughput: %u templates in %.3f s (%.1f templates/s, setup %.3f s)\n",
                 res.templates_run, res.t_templates, res.templates_run / std::max(res.t_templates, 1e-9), res.t_setup);
   }
-  if (rc == 0 && res.interrupted) boinc::finish(0);
+  // quit / abort / lost heartbeat: leave without a final checkpoint and
+  // without the finish marker (demod_binary.c:1489-1492 calls exit(0))
+  if (rc == 0 && res.interrupted) boinc::quit_exit(0);
   return rc;
 }
 
@@ -286,7 +288,7 @@ int wrapper_main(int argc, char** argv) {
       case 'v':
         log_message(LOG_INFO, true, "Version information:\n");
         log_message(LOG_INFO, false, "Binary Pulsar Search Revision: %s\n", BRP_GIT_ID);
-        log_message(LOG_INFO, false, "BOINC Revision: %s\n", "standalone-shim");
+        log_message(LOG_INFO, false, "BOINC Revision: %s\n", "brp-app-runtime (client shared memory protocol)");
         return 0;
       case 1001: fwd.push_back("--mi355x-batch"); fwd.push_back(optarg); break;
       case 1002: fwd.push_back("--mi355x-gpus"); fwd.push_back(optarg); break;
@@ -329,6 +331,7 @@ int wrapper_main(int argc, char** argv) {
     std::vector<char*> av;
     for (auto& s : args) av.push_back(const_cast<char*>(s.c_str()));
     av.push_back(nullptr);
+    boinc::set_pass(static_cast<int>(pass), static_cast<int>(passes));
     result = search_main(static_cast<int>(args.size()), av.data());
     if (result) {
       log_message(LOG_ERROR, true, "Demodulation failed (error: %i)!\n", result);

@@ -14,7 +14,7 @@
 #include <set>
 #include <thread>
 
-#include "../boinc/boinc_shim.hpp"
+#include "../boinc/runtime.hpp"
 #include "../boinc/ipc.hpp"
 #include "../core/errors.hpp"
 #include "../core/fault.hpp"
@@ -125,7 +125,7 @@ int finalize_output(const SearchOptions& opt, const SearchGeometry& g, uint32_t 
   if (slash != std::string::npos) ex = ex.substr(slash + 1);
   info.exec_name = ex;
   info.git_id = BRP_GIT_ID;
-  info.boinc_rev = "standalone-shim";
+  info.boinc_rev = boinc::is_standalone() ? "standalone" : "brp-app-runtime";
   CPCand cands[kCandTotal];
   std::memcpy(cands, table.data(), sizeof(cands));
   return write_results(opt.outputfile, cands, g.t_obs_d, info);
@@ -303,6 +303,9 @@ int SearchSession::run(uint32_t begin, uint32_t end, CandidateTable& table, Sear
   std::atomic<bool> stop{false};
   auto worker = [&](Backend* be) {
     for (;;) {
+      // a suspended task starts no GPU work; batches already launched
+      // finish inside their critical section (demod_binary.c:1241-1296)
+      boinc::suspend_point();
       if (stop.load()) return;
       const uint32_t first = next_first.fetch_add(static_cast<uint32_t>(B));
       if (first >= end) return;
@@ -314,7 +317,9 @@ int SearchSession::run(uint32_t begin, uint32_t end, CandidateTable& table, Sear
       }
       BatchResult br;
       br.first = first;
+      boinc::begin_critical_section();
       br.rc = be->process(&d.tin[first], n, thr, br.cands);
+      boinc::end_critical_section();
       {
         std::lock_guard<std::mutex> lk(mu);
         ready.emplace(first, std::move(br));
@@ -389,6 +394,7 @@ int run_search(const SearchOptions& opt, const SearchControl& ctl, SearchResult&
   const double t_start = now_s();
   res = SearchResult();
   log_message(LOG_INFO, true, "Starting data processing...\n");
+  if (fault_enabled("resource_error")) return RADPUL_HIP_MEM_ALLOC_HOST;
   SearchSession session;
   int rc = session.open(opt, ctl);
   if (rc) return rc;
@@ -454,9 +460,12 @@ int run_search(const SearchOptions& opt, const SearchControl& ctl, SearchResult&
   res.t_setup = now_s() - t_start;
 
   const double t_loop = now_s();
-  long kill_after = -1;
+  long kill_after = -1, segv_after = -1;
   std::string fault_arg;
   if (fault_enabled("kill_after_template", &fault_arg)) kill_after = std::atol(fault_arg.c_str());
+  if (fault_enabled("segv_after_template", &fault_arg)) segv_after = std::atol(fault_arg.c_str());
+  long slow_ms = 0;
+  if (fault_enabled("slow_template", &fault_arg)) slow_ms = std::atol(fault_arg.c_str());
   int cp_rc = 0;
   auto hook = [&](uint32_t done, const SearchInfo& info) -> bool {
     counter = done;
@@ -473,11 +482,22 @@ int run_search(const SearchOptions& opt, const SearchControl& ctl, SearchResult&
       std::memcpy(cp.cands, table.data(), sizeof(cp.cands));
       trace::Range range("brp:checkpoint");
       cp_rc = write_checkpoint(opt.checkpointfile, cp);
-      if (cp_rc) return false;
+      if (cp_rc) {
+        boinc::end_critical_section();
+        return false;
+      }
       log_message(LOG_INFO, true, "Checkpoint committed!\n");
       boinc::checkpoint_completed();
     }
     if (kill_after >= 0 && counter >= static_cast<uint32_t>(kill_after)) boinc::request_quit();
+    if (segv_after >= 0 && counter >= static_cast<uint32_t>(segv_after)) {
+      // a real invalid store (not raise()) so the crash report shows this frame
+      static volatile uintptr_t no_page = 0;
+      *reinterpret_cast<volatile int*>(no_page) = 1;
+    }
+    if (slow_ms > 0) std::this_thread::sleep_for(std::chrono::milliseconds(slow_ms));
+    // template boundary: a suspended task waits here (no GPU work is queued)
+    boinc::suspend_point();
     const boinc::Status st = boinc::get_status();
     return !(st.quit_request || st.abort_request || st.no_heartbeat);
   };

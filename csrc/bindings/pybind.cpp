@@ -9,7 +9,7 @@
 
 #include "../app/multi.hpp"
 #include "../app/search.hpp"
-#include "../boinc/boinc_shim.hpp"
+#include "../boinc/runtime.hpp"
 #include "../boinc/ipc.hpp"
 #include "../core/cpu_backend.hpp"
 #include "../core/cpu_fft.hpp"

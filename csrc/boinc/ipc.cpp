@@ -5,7 +5,7 @@
 #include <iomanip>
 #include <sstream>
 
-#include "boinc_shim.hpp"
+#include "runtime.hpp"
 
 namespace brp {
 namespace ipc {

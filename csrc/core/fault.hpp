@@ -8,6 +8,10 @@
 //   kill_after_template:N  request a BOINC quit once N templates are done
 //   hip_oom                every device allocation fails (-> temporary exit)
 //   pinned_fail            every pinned host allocation fails (-> pageable)
+//   segv_after_template:N  invalid store once N templates are done (crash report)
+//   slow_template:MS       sleep MS ms per applied template (paces client tests)
+//   resource_error         the search returns a host allocation failure
+//                          (-> BOINC temporary exit)
 //   collective_timeout[:R] rank R (default 1) stalls before the all-gather
 //                          (Python side, parallel/dist.py)
 #pragma once
