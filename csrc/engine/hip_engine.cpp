@@ -208,6 +208,10 @@ struct HipEngine::Impl {
   int hs_stage = 0;
   uint32_t hs_xcd = 0;          // BRP_HS_XCD=1: XCD-contiguous harmonic-sum tiles
   uint32_t hs_tile = 0;         // harmonic-sum bins per workgroup (wisdom / BRP_HS_TILE, 0 = kHsTile)
+  // harmonic-sum kernel: per-i gathers (default), or the measured-equal /
+  // slower register-blocked layouts (BRP_HS_KERNEL=quad / rb, fp32 spectrum only)
+  int hs_variant = hipk::HS_GATHER;
+  int hs_rb_occ = 0;
   uint32_t persist_per_cu = 4;  // persistent FFT passes: workgroups per CU (BRP_PERSIST, 0 = off)
   uint32_t ps_stride = 0;
   uint32_t i_start = 0;
@@ -460,6 +464,8 @@ struct HipEngine::Impl {
         ah.staged_harmonics = hs_stage;
         ah.tile = hs_tile;
         ah.xcd = hs_xcd;
+        ah.variant = ps_fp16 ? hipk::HS_GATHER : hs_variant;
+        ah.rb_occupancy = hs_rb_occ;
         return hipk::launch_harmonic_sum(ah, nb, stream);
       }
       case kEpilogue:
@@ -636,6 +642,13 @@ int HipEngine::setup(const SearchGeometry& g, const std::vector<float>& series, 
   if (const char* e = std::getenv("BRP_HS_TILE")) d.hs_tile = static_cast<uint32_t>(std::atoi(e));
   if (const char* e = std::getenv("BRP_HS_XCD")) d.hs_xcd = static_cast<uint32_t>(std::atoi(e));
   if (d.hs_stage != 0) d.hs_tile = hipk::kHsTile;  // the LDS staging layout is built for the default tile
+  d.hs_variant = hipk::HS_GATHER;
+  if (const char* e = std::getenv("BRP_HS_KERNEL"))
+    d.hs_variant = std::strcmp(e, "rb") == 0 ? hipk::HS_REGISTER_BLOCKED
+                   : std::strcmp(e, "quad") == 0 ? hipk::HS_QUAD
+                                                 : hipk::HS_GATHER;
+  if (d.hs_stage != 0 || d.hs_xcd != 0) d.hs_variant = hipk::HS_GATHER;
+  if (const char* e = std::getenv("BRP_HS_RB_OCC")) d.hs_rb_occ = std::atoi(e);
   d.plan.persist_wgs = d.persist_per_cu * d.num_cus;
   // opt-in (BRP_FFT2=1): measured 84 vs 78 us/template sequential, the
   // three-pass kernels keep more workgroups per CU (profiles/README.md)

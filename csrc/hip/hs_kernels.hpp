@@ -10,7 +10,15 @@ namespace hipk {
 
 constexpr int kHsTile = 1024;  // fundamental-level bins i per workgroup
 
+enum HSVariant : int {
+  HS_GATHER = 0,            // one lane per i, 16 gathers (tiles + halo, LDS level maxima)
+  HS_REGISTER_BLOCKED = 1,  // one lane per 16 i, 16 contiguous runs per lane (fp32 spectrum)
+  HS_QUAD = 2,              // one lane per 4 i, one 16-byte load per harmonic (fp32 spectrum)
+};
+
 struct HSArgs {
+  int variant;            // HSVariant
+  int rb_occupancy;       // register-blocked kernel: minimum waves per SIMD the compiler targets (0 = free)
   const float* ps;        // [batch][ps_stride]
   const _Float16* ps16;   // fp16 spectrum (config 5) instead of `ps` when non-null
   uint32_t ps_stride;
@@ -34,6 +42,7 @@ __host__ __device__ constexpr uint32_t hs_pack(uint32_t k, uint32_t h, uint32_t 
 }
 
 uint32_t hs_num_tiles(uint32_t i_start, uint32_t hhi, uint32_t tile = kHsTile);
+uint32_t hs_rb_num_groups(uint32_t w2, uint32_t hhi);
 hipError_t launch_harmonic_sum(const HSArgs& a, int batch, hipStream_t s);
 
 }  // namespace hipk

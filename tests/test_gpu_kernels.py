@@ -60,12 +60,16 @@ def test_power_spectrum_bench_size(brp, gpu):
         assert err.max() < 1e-3, (k, err.max(), int(np.argmax(err)) + 1)
 
 
-def test_harmonic_sum_matches_cpu_bitwise(brp, gpu, tmp_path):
-    """Same power spectrum in -> identical candidate bins and powers out."""
+@pytest.mark.parametrize("variant,window", [("rb", 100), ("rb", 10), ("rb", 1001), ("gather", 100), ("quad", 100), ("quad", 1001)])
+def test_harmonic_sum_matches_cpu_bitwise(brp, gpu, tmp_path, monkeypatch, variant, window):
+    """Same power spectrum in -> identical candidate bins and powers out, for the
+    register-blocked kernel (default; windows below 8 and odd ones included)
+    and the per-i gather kernel."""
+    monkeypatch.setenv("BRP_HS_KERNEL", variant)
     case = synth.synthetic_case(tmp_path, n=1 << 17, n_templates=2,
                                 inj=synth.Injection(f0=150.0, P_orb=900.0, tau=0.02, psi0=2.0, amplitude=3.0))
     hdr, series, _ = brp.read_work_unit(case["wu"])
-    geom = brp.derive_geometry(hdr, dict(f0=120.0, padding=3.0, fA=0.08, window=100))
+    geom = brp.derive_geometry(hdr, dict(f0=120.0, padding=3.0, fA=0.08, window=window))
     eng = _engine(brp, geom, series, batch=1)
     P, tau, psi = (np.float32(case[key][0]) for key in ("P", "tau", "psi"))
     thr = [4.0, 6.0, 9.0, 14.0, 24.0]  # low thresholds -> many candidates
@@ -78,6 +82,28 @@ def test_harmonic_sum_matches_cpu_bitwise(brp, gpu, tmp_path):
         assert len(bins_c) > 0
         np.testing.assert_array_equal(bins_g, bins_c)
         np.testing.assert_array_equal(pw_g, pw_c)
+
+
+@pytest.mark.parametrize("variant", ["rb", "quad", "gather"])
+def test_harmonic_sum_bench_size_matches_cpu_bitwise(brp, gpu, monkeypatch, variant):
+    """Benchmark geometry (hhi = 5.27 M bins, two templates of a batch): every
+    harmonic-sum kernel's candidates equal the CPU model's on the same spectrum."""
+    monkeypatch.setenv("BRP_HS_KERNEL", variant)
+    hdr, series, _ = brp.read_work_unit(str(WU))
+    opt = dict(OPT_BENCH, white=True)
+    geom = brp.derive_geometry(hdr, opt)
+    eng = _engine(brp, geom, series, batch=2)
+    series = eng.whiten(opt, brp.read_zaplist(str(ZAP)), series)
+    P, tau, psi = brp.read_template_bank(str(BANK))
+    thr = [9.0, 12.0, 16.0, 22.0, 33.0]
+    outs = eng.process(P[:2].astype(np.float32), tau[:2].astype(np.float32), psi[:2].astype(np.float32), thr)
+    for k in range(2):
+        ps_gpu, _ = eng.power_spectrum(float(np.float32(P[k])), float(np.float32(tau[k])), float(np.float32(psi[k])))
+        ref, _ = brp.cpu_harmonic_sum(ps_gpu, geom, thr)
+        for h in range(5):
+            assert len(ref[h][0]) > 0
+            np.testing.assert_array_equal(outs[k][h][0], ref[h][0])
+            np.testing.assert_array_equal(outs[k][h][1], ref[h][1])
 
 
 def test_whitening_matches_cpu(brp, gpu, tmp_path):
