@@ -33,7 +33,7 @@ HOST_SRCS = [
     "core/search_core.cpp", "core/cpu_fft.cpp", "core/cpu_backend.cpp", "core/wisdom.cpp", "core/trace.cpp",
     "boinc/runtime.cpp", "boinc/crash.cpp", "boinc/ipc.cpp",
     "engine/cpu_engine.cpp", "engine/hip_engine.cpp",
-    "app/search.cpp", "app/multi.cpp", "app/cli.cpp",
+    "app/search.cpp", "app/multi.cpp", "app/passes.cpp", "app/cli.cpp",
 ]
 DEVICE_SRCS = [
     "hip/fft_passes.hip", "hip/fft2.hip", "hip/harmonic_sum.hip", "hip/resample.hip", "hip/whiten.hip",

@@ -32,9 +32,10 @@ class MultiWUSearch:
         self.total = self.session.total()
         self.timings: dict = {}
 
-    def step(self, limit: int | None = None):
+    def step(self, limit: int | None = None, block_batches: int = 0):
         """Whiten every WU, search this rank's share of the bank for all WUs,
-        all-gather and merge. Returns one candidate table per WU."""
+        all-gather and merge. Returns one candidate table per WU.
+        `block_batches` overrides the WU-major deal block (batches per block)."""
         from ..parallel.dist import sharded_merge
 
         total = self.total if limit is None else min(limit, self.total)
@@ -45,7 +46,7 @@ class MultiWUSearch:
 
         def run_shard(begin, end):
             ts = time.perf_counter()
-            tables, _ = self.session.run(begin, end)
+            tables, _ = self.session.run(begin, end, block_batches)
             search_s[0] += time.perf_counter() - ts
             return tables
 

@@ -47,6 +47,7 @@ void print_usage(const char* prog) {
   std::printf(" --mi355x-pipelines\t\tinteger\tIndependent pipelines per GPU (default 3, one template each).\n");
   std::printf(" --mi355x-no-checkpoint\t\tboolean\tNever read or write checkpoints (Debian NOCHECKPOINTING build).\n");
   std::printf(" --mi355x-progress-every\tinteger\tReport fraction done every N templates (Debian COMMUNICATIONREDUCTION).\n");
+  std::printf(" --mi355x-sequential-passes\tboolean\tRun several -i/-o pairs one after another instead of batched.\n");
   std::printf("\n");
 }
 
@@ -54,10 +55,10 @@ bool is(const char* a, const char* s, const char* l) { return std::strcmp(a, s) 
 
 }  // namespace
 
-int search_main(int argc, char** argv) {
-  SearchOptions opt;
-  bool spin = false;  // --mi355x-spin: busy-wait host synchronisation
-  SearchControl ctl;
+int parse_search_args(int argc, char** argv, SearchOptions& opt, SearchControl& ctl, bool& spin) {
+  opt = SearchOptions();
+  ctl = SearchControl();
+  spin = false;  // --mi355x-spin: busy-wait host synchronisation
   // measured best on one MI355X: 3 pipelines of one template each (the FFT
   // intermediates of every pipeline stay in the Infinity Cache)
   ctl.pipelines = 3;
@@ -212,6 +213,15 @@ int search_main(int argc, char** argv) {
     log_message(LOG_ERROR, true, "Disabled checkpointing - '-c %s' option ignored\n", opt.checkpointfile.c_str());
     opt.checkpointfile.clear();
   }
+  return 0;
+}
+
+int search_main(int argc, char** argv) {
+  SearchOptions opt;
+  SearchControl ctl;
+  bool spin = false;
+  int prc = parse_search_args(argc, argv, opt, ctl, spin);
+  if (prc) return prc;
   // a BOINC app shares the host: wait for the GPU by sleeping, as the
   // reference's blocking-sync context does, unless --mi355x-spin
   hip_set_blocking_sync(!spin);
@@ -231,6 +241,7 @@ int wrapper_main(int argc, char** argv) {
   std::vector<std::string> fwd;       // forwarded options (short forms)
   std::vector<std::string> inputs, outputs;
   std::string checkpoint;
+  bool sequential = false;  // --mi355x-sequential-passes
   fwd.push_back(argv[0]);
   static struct option long_options[] = {{"input-file", required_argument, 0, 'i'},
                                          {"template-bank-file", required_argument, 0, 't'},
@@ -255,6 +266,7 @@ int wrapper_main(int argc, char** argv) {
                                          {"mi355x-pipelines", required_argument, 0, 1006},
                                          {"mi355x-no-checkpoint", no_argument, 0, 1007},
                                          {"mi355x-progress-every", required_argument, 0, 1008},
+                                         {"mi355x-sequential-passes", no_argument, 0, 1009},
                                          {0, 0, 0, 0}};
   optind = 1;
   auto file_arg = [&](const char* opt, const char* val) {
@@ -298,6 +310,7 @@ int wrapper_main(int argc, char** argv) {
       case 1006: fwd.push_back("--mi355x-pipelines"); fwd.push_back(optarg); break;
       case 1007: fwd.push_back("--mi355x-no-checkpoint"); break;
       case 1008: fwd.push_back("--mi355x-progress-every"); fwd.push_back(optarg); break;
+      case 1009: sequential = true; break;
       default: boinc::finish(EINSTEINRADIO_EOPT);
     }
   }
@@ -314,6 +327,40 @@ int wrapper_main(int argc, char** argv) {
     log_message(LOG_WARN, true, "Shared memory setup failed!\n");
   }
   const size_t passes = inputs.size();
+  // several pending same-shape passes on the HIP backend: one batched session
+  // holds every pending WU in HBM (csrc/app/passes.cpp); otherwise, and for
+  // passes it cannot batch, the reference's sequential loop below
+  if (!result && passes >= 2 && !sequential) {
+    std::vector<std::string> in_phys(passes), out_phys(passes);
+    std::vector<size_t> pending;
+    for (size_t p = 0; p < passes; ++p) {
+      boinc::resolve_filename(inputs[p], in_phys[p]);
+      boinc::resolve_filename(outputs[p], out_phys[p]);
+      if (FILE* fp = std::fopen(out_phys[p].c_str(), "r")) {
+        log_message(LOG_INFO, true, "Output file: '%s' already exists - skipping pass\n", out_phys[p].c_str());
+        std::fclose(fp);
+      } else {
+        pending.push_back(p);
+      }
+    }
+    std::vector<char*> av;
+    for (auto& a : fwd) av.push_back(const_cast<char*>(a.c_str()));
+    av.push_back(nullptr);
+    SearchOptions opt;
+    SearchControl ctl;
+    bool spin = false;
+    if (pending.size() >= 2 && parse_search_args(static_cast<int>(fwd.size()), av.data(), opt, ctl, spin) == 0 &&
+        !opt.use_cpu) {
+      hip_set_blocking_sync(!spin);
+      bool fallback = false;
+      result = run_passes_batched(in_phys, out_phys, pending, opt, ctl, fallback);
+      if (!fallback) {
+        if (result) log_message(LOG_ERROR, true, "Demodulation failed (error: %i)!\n", result);
+        return result;
+      }
+      log_message(LOG_INFO, true, "Work units differ in shape: processing the passes one after another.\n");
+    }
+  }
   for (size_t pass = 0; pass < passes && !result; ++pass) {
     std::vector<std::string> args = fwd;
     std::string in_phys, out_phys;

@@ -10,6 +10,7 @@
 #include <mutex>
 #include <thread>
 
+#include "../boinc/runtime.hpp"
 #include "../core/errors.hpp"
 #include "../core/io.hpp"
 #include "../core/log.hpp"
@@ -31,6 +32,13 @@ bool same_shape(const SearchGeometry& a, const SearchGeometry& b) {
          a.harmonic_idx_hi == b.harmonic_idx_hi && a.dt == b.dt && a.step_inv == b.step_inv;
 }
 
+// TB = B * batches in 64 bits, clamped to the bank rounded up to whole batches
+uint32_t multi_block_templates_for(int B, uint32_t total, uint64_t batches) {
+  const uint64_t b = static_cast<uint64_t>(std::max(1, B));
+  const uint64_t cap = std::max<uint64_t>(b, (static_cast<uint64_t>(total) + b - 1) / b * b);
+  return static_cast<uint32_t>(std::min<uint64_t>(b * std::max<uint64_t>(1, batches), cap));
+}
+
 }  // namespace
 
 struct MultiSession::Impl {
@@ -42,13 +50,27 @@ struct MultiSession::Impl {
   std::vector<ZapRange> zaps;
   std::vector<std::unique_ptr<HipEngine>> engines;
   std::vector<std::string> inputs;
+  uint32_t block_batches = 0;  // 0: BRP_MULTI_BLOCK / default
+  bool shape_mismatch = false;
+  SearchInfo info;
 };
+
+uint32_t multi_block_templates(int B, uint32_t total) {
+  static const uint64_t env_batches = [] {
+    const char* e = std::getenv("BRP_MULTI_BLOCK");
+    return e ? static_cast<uint64_t>(std::max(1L, std::atol(e))) : 64ull;
+  }();
+  return multi_block_templates_for(B, total, env_batches);
+}
 
 MultiSession::MultiSession() : impl_(new Impl) {}
 MultiSession::~MultiSession() = default;
 size_t MultiSession::work_units() const { return impl_->wus.size(); }
 uint32_t MultiSession::total() const { return static_cast<uint32_t>(impl_->bank.size()); }
 const SearchGeometry& MultiSession::geometry() const { return impl_->geoms.at(0); }
+void MultiSession::set_block_batches(uint32_t n) { impl_->block_batches = n; }
+const SearchInfo& MultiSession::info() const { return impl_->info; }
+bool MultiSession::shape_mismatch() const { return impl_->shape_mismatch; }
 
 BackendStats MultiSession::stats() const {
   BackendStats t;
@@ -59,6 +81,7 @@ BackendStats MultiSession::stats() const {
     t.templates += s.templates;
     t.batches += s.batches;
     t.overflow_reruns += s.overflow_reruns;
+    t.shared_series_batches += s.shared_series_batches;
   }
   return t;
 }
@@ -84,11 +107,13 @@ int MultiSession::open(const std::vector<std::string>& inputs, const SearchOptio
     if ((rc = read_work_unit(inputs[k], d.wus[k]))) return rc;
     if ((rc = derive_geometry(d.wus[k].header, opt, d.geoms[k]))) return rc;
     if (!same_shape(d.geoms[k], d.geoms[0])) {
-      log_message(LOG_ERROR, true, "Work unit %s differs in shape from %s; batch only same-shape WUs.\n",
+      log_message(LOG_WARN, true, "Work unit %s differs in shape from %s; batch only same-shape WUs.\n",
                   inputs[k].c_str(), inputs[0].c_str());
+      d.shape_mismatch = true;
       return RADPUL_EVAL;
     }
   }
+  sky_position(d.wus[0].header, d.info);
   if (!hip_backend_supports(d.geoms[0])) {
     log_message(LOG_ERROR, true, "No HIP FFT plan for N = %u.\n", d.geoms[0].nsamples);
     return RADPUL_HIP_FFT_PLAN;
@@ -146,15 +171,21 @@ int MultiSession::prepare() {
 }
 
 int MultiSession::run(uint32_t begin, uint32_t end, std::vector<CandidateTable>& tables, MultiResult& res) {
+  return run(std::vector<uint32_t>(impl_->wus.size(), begin), end, tables, res, MultiHook());
+}
+
+int MultiSession::run(const std::vector<uint32_t>& begins, uint32_t end, std::vector<CandidateTable>& tables,
+                      MultiResult& res, const MultiHook& hook) {
   Impl& d = *impl_;
   trace::Range range("brp:multi_templates");
   const SearchGeometry& g = d.geoms[0];
   const uint32_t K = static_cast<uint32_t>(d.wus.size());
+  if (begins.size() != K) return RADPUL_EVAL;
   end = std::min<uint32_t>(end == 0 ? total() : end, total());
   tables.resize(K);
+  const uint32_t begin = *std::min_element(begins.begin(), begins.end());
   if (begin >= end) return 0;
   const double t0 = now_s();
-  const uint64_t npairs = static_cast<uint64_t>(end - begin) * K;
   const int B = d.engines[0]->batch();
   // device thresholds per WU (lag by the batches in flight; exact ones on the host)
   std::vector<float> thr_wu(static_cast<size_t>(K) * kNumHarmonicLevels);
@@ -175,16 +206,19 @@ int MultiSession::run(uint32_t begin, uint32_t end, std::vector<CandidateTable>&
   // templates in increasing order. Long blocks keep all pipelines on the same
   // WU, so one 16 MB series (not K of them) competes with the pipelines' FFT
   // buffers for the 256 MB Infinity Cache. BRP_MULTI_BLOCK = batches per block.
-  static const uint32_t block_batches = [] {
-    const char* e = std::getenv("BRP_MULTI_BLOCK");
-    return e ? std::max(1, std::atoi(e)) : 64;
-  }();
-  const uint32_t TB = static_cast<uint32_t>(B) * block_batches;
+  const uint32_t TB = d.block_batches ? multi_block_templates_for(B, end - begin, d.block_batches)
+                                       : multi_block_templates(B, end - begin);
   std::vector<std::pair<uint32_t, uint32_t>> order;  // (template, WU)
-  order.reserve(npairs);
-  for (uint32_t t0 = begin; t0 < end; t0 += TB)
+  // deal blocks: end index in `order` and the template prefix complete after it
+  std::vector<std::pair<uint64_t, uint32_t>> blocks;
+  for (uint64_t t0 = begin; t0 < end; t0 += TB) {
+    const uint32_t t_hi = static_cast<uint32_t>(std::min<uint64_t>(t0 + TB, end));
     for (uint32_t w = 0; w < K; ++w)
-      for (uint32_t t = t0; t < std::min<uint32_t>(t0 + TB, end); ++t) order.emplace_back(t, w);
+      for (uint32_t t = std::max<uint32_t>(static_cast<uint32_t>(t0), begins[w]); t < t_hi; ++t) order.emplace_back(t, w);
+    blocks.emplace_back(order.size(), t_hi);
+  }
+  const uint64_t npairs = order.size();
+  if (npairs == 0) return 0;
   auto pair_input = [&](uint64_t q) {
     const uint32_t t = order[q].first;
     const uint32_t w = order[q].second;
@@ -196,6 +230,7 @@ int MultiSession::run(uint32_t begin, uint32_t end, std::vector<CandidateTable>&
   auto worker = [&](HipEngine* eng) {
     std::vector<float> thr;
     for (;;) {
+      boinc::suspend_point();  // no GPU work starts while the client has the task suspended
       if (stop.load()) return;
       const uint64_t first = next.fetch_add(static_cast<uint64_t>(B));
       if (first >= npairs) return;
@@ -211,7 +246,9 @@ int MultiSession::run(uint32_t begin, uint32_t end, std::vector<CandidateTable>&
                       &thr_wu[static_cast<size_t>(bt.tin[i].wu) * kNumHarmonicLevels],
                       sizeof(float) * kNumHarmonicLevels);
       }
+      boinc::begin_critical_section();
       bt.rc = eng->process(bt.tin.data(), n, thr.data(), kNumHarmonicLevels, bt.cands);
+      boinc::end_critical_section();
       {
         std::lock_guard<std::mutex> lk(mu);
         ready.emplace(first, std::move(bt));
@@ -222,6 +259,7 @@ int MultiSession::run(uint32_t begin, uint32_t end, std::vector<CandidateTable>&
   std::vector<std::thread> threads;
   for (auto& e : d.engines) threads.emplace_back(worker, e.get());
   uint64_t applied = 0;
+  size_t next_block = 0;
   int rc = 0;
   while (applied < npairs) {
     Batch bt;
@@ -250,6 +288,18 @@ int MultiSession::run(uint32_t begin, uint32_t end, std::vector<CandidateTable>&
     {
       std::lock_guard<std::mutex> lk(mu);
       for (uint32_t w = 0; w < K; ++w) tables[w].thresholds(d.geoms[w].chi2_thr, &thr_wu[w * kNumHarmonicLevels]);
+    }
+    if (!bt.tin.empty()) {
+      const TemplateInput& last = bt.tin.back();
+      d.info.orbital_radius = last.tau;
+      d.info.orbital_period = last.P;
+      d.info.orbital_phase = last.Psi0;
+    }
+    uint32_t prefix = 0;
+    while (next_block < blocks.size() && applied >= blocks[next_block].first) prefix = blocks[next_block++].second;
+    if (hook && !hook(applied, prefix)) {
+      res.interrupted = true;
+      break;
     }
   }
   stop.store(true);

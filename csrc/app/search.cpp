@@ -36,6 +36,8 @@ double now_s() {
   return duration<double>(steady_clock::now().time_since_epoch()).count();
 }
 
+}  // namespace
+
 // RA/DEC (hhmmss.s / ddmmss.s) to radians for the screensaver (demod_binary.c:745-771)
 void sky_position(const DDHeader& h, SearchInfo& info) {
   float hrs = std::floor(h.RA / 10000.0);
@@ -55,6 +57,8 @@ void sky_position(const DDHeader& h, SearchInfo& info) {
   }
   info.dispersion_measure = h.DM;
 }
+
+namespace {
 
 void log_header(const DDHeader& h) {
   log_message(LOG_INFO, true, "Header contents:\n");
@@ -163,6 +167,7 @@ BackendStats SearchSession::stats() const {
     t.templates += s.templates;
     t.batches += s.batches;
     t.overflow_reruns += s.overflow_reruns;
+    t.shared_series_batches += s.shared_series_batches;
   }
   return t;
 }

@@ -65,6 +65,9 @@ class SearchSession {
   std::unique_ptr<Impl> impl_;
 };
 
+// Screensaver sky position / DM of a WU header (demod_binary.c:745-771).
+void sky_position(const DDHeader& h, SearchInfo& info);
+
 // Full search of one WU with the options' files. Returns a RADPUL_* code.
 int run_search(const SearchOptions& opt, const SearchControl& ctl, SearchResult& res);
 
@@ -72,6 +75,18 @@ int run_search(const SearchOptions& opt, const SearchControl& ctl, SearchResult&
 // the --input_file style long names, demod_binary.c:217-445) plus MI355X
 // extensions (--mi355x-batch N, --mi355x-gpus N, --mi355x-cpu).
 int search_main(int argc, char** argv);
+
+// Parse the MAIN command line (plus --mi355x-* extensions) into options.
+int parse_search_args(int argc, char** argv, SearchOptions& opt, SearchControl& ctl, bool& spin);
+
+// Batched multi-pass task: the pending passes (indices into in/out) run as one
+// MultiSession with per-WU checkpoints "<cp>.<pass>", results and reference
+// pass semantics. Sets `fallback` (and returns 0) when the WUs cannot be
+// batched (different shapes, no HIP FFT plan); the caller then runs the passes
+// sequentially.
+int run_passes_batched(const std::vector<std::string>& in, const std::vector<std::string>& out,
+                       const std::vector<size_t>& pending, const SearchOptions& opt, const SearchControl& ctl,
+                       bool& fallback);
 
 // BOINC wrapper entry (erp_boinc_wrapper.cpp:242-584): getopt_long with the
 // dashed long names, several -i/-o pairs processed as sequential passes.

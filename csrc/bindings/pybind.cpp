@@ -450,6 +450,7 @@ PYBIND11_MODULE(_brp, m) {
              }
              return cands_to_list(out);
            })
+      .def("adopt_series", [](HipEngine& e, const HipEngine& src) { check(e.adopt_series(src), "HipEngine.adopt_series"); })
       .def("power_spectrum",
            [](HipEngine& e, float P, float tau, float psi) {
              std::vector<float> ps;
@@ -483,6 +484,7 @@ PYBIND11_MODULE(_brp, m) {
         d["templates"] = s.templates;
         d["batches"] = s.batches;
         d["overflow_reruns"] = s.overflow_reruns;
+        d["shared_series_batches"] = s.shared_series_batches;
         return d;
       });
   m.def("fft_plan", [](uint32_t M) -> py::object {
@@ -571,6 +573,7 @@ PYBIND11_MODULE(_brp, m) {
         d["templates"] = st.templates;
         d["batches"] = st.batches;
         d["overflow_reruns"] = st.overflow_reruns;
+        d["shared_series_batches"] = st.shared_series_batches;
         return d;
       });
   py::class_<MultiSession>(m, "MultiSession")
@@ -596,12 +599,13 @@ PYBIND11_MODULE(_brp, m) {
            })
       .def(
           "run",
-          [](MultiSession& s, uint32_t begin, uint32_t end) {
+          [](MultiSession& s, uint32_t begin, uint32_t end, uint32_t block_batches) {
             std::vector<CandidateTable> tables;
             MultiResult res;
             int rc;
             {
               py::gil_scoped_release rel;
+              s.set_block_batches(block_batches);
               rc = s.run(begin, end, tables, res);
             }
             check(rc, "MultiSession.run");
@@ -610,7 +614,7 @@ PYBIND11_MODULE(_brp, m) {
             d["t_templates"] = res.t_templates;
             return py::make_tuple(tables, d);
           },
-          py::arg("begin") = 0, py::arg("end") = 0)
+          py::arg("begin") = 0, py::arg("end") = 0, py::arg("block_batches") = 0)
       .def("finalize",
            [](MultiSession& s, std::vector<std::string> outputs, uint32_t n_done, std::vector<CandidateTable> tables) {
              check(s.finalize(outputs, n_done, tables), "MultiSession.finalize");

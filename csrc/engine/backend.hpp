@@ -29,6 +29,7 @@ struct BackendStats {
   uint64_t templates = 0;
   uint64_t batches = 0;
   uint64_t overflow_reruns = 0;
+  uint64_t shared_series_batches = 0;  // batches that read another pipeline's series in place
 };
 
 class Backend {

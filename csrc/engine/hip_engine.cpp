@@ -228,10 +228,24 @@ struct HipEngine::Impl {
   // one copy for all pipelines keeps the Infinity-Cache footprint down
   const float* shared_series = nullptr;
   const float* series_in() const { return shared_series != nullptr ? shared_series : series.p; }
+  // Generation of this engine's own series buffer: bumped whenever it is
+  // reallocated, rewritten or freed. An engine reading it in place holds the
+  // token (which outlives this engine) and the generation it adopted, and
+  // refuses to launch once they differ (the source was set up again, whitened
+  // another WU or destroyed before the reader was set up again).
+  std::shared_ptr<std::atomic<uint64_t>> series_token = std::make_shared<std::atomic<uint64_t>>(0);
+  std::shared_ptr<std::atomic<uint64_t>> adopted_token;
+  uint64_t adopted_gen = 0;
+  void bump_series() { series_token->fetch_add(1); }
+  bool shared_series_valid() const {
+    return shared_series == nullptr || (adopted_token && adopted_token->load() == adopted_gen);
+  }
   // back to the engine's own series (before anything writes it)
   void own_series() {
+    bump_series();
     if (shared_series == nullptr) return;
     shared_series = nullptr;
+    adopted_token.reset();
     for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second);  // captured series pointer changed
     graphs.clear();
   }
@@ -340,6 +354,7 @@ struct HipEngine::Impl {
   }
 
   ~Impl() {
+    bump_series();  // readers of this series must not launch any more
     for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second);
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
@@ -754,6 +769,13 @@ int HipEngine::adopt_series(const HipEngine& src) {
     for (auto& kv : d.graphs) (void)hipGraphExecDestroy(kv.second);  // captured series pointer changed
     d.graphs.clear();
   }
+  if (want != nullptr) {
+    // the source may itself read a third engine's series: follow that token
+    d.adopted_token = s.shared_series != nullptr ? s.adopted_token : s.series_token;
+    d.adopted_gen = s.shared_series != nullptr ? s.adopted_gen : s.series_token->load();
+  } else {
+    d.adopted_token.reset();
+  }
   if (!share)
     BRP_HIP_CHECK(hipMemcpy(d.series.p, s.series.p, d.g.n_unpadded * sizeof(float), hipMemcpyDeviceToDevice),
                   RADPUL_HIP_MEM_COPY_HOST_DEVICE);
@@ -766,6 +788,7 @@ int HipEngine::set_slots(uint32_t k) {
   if (k != d.slots) {
     d.slots = k;
     d.ready = false;  // the next setup() reallocates the series buffer
+    d.bump_series();
   }
   return 0;
 }
@@ -950,6 +973,10 @@ int HipEngine::process(const TemplateInput* t, int n, const float* thr, int thr_
                        std::vector<TemplateCands>& out) {
   Impl& d = *impl_;
   if (!d.ready) return RADPUL_EMISC;
+  if (!d.shared_series_valid()) {
+    log_message(LOG_ERROR, true, "Pipeline reads a whitened series that was rewritten or freed since it was adopted.\n");
+    return RADPUL_EVAL;
+  }
   BRP_HIP_CHECK(hipSetDevice(d.device), RADPUL_HIP_DEVICE_SET);  // worker threads drive their own device
   out.clear();
   out.resize(n);
@@ -1008,6 +1035,7 @@ int HipEngine::process(const TemplateInput* t, int n, const float* thr, int thr_
     (void)hipEventElapsedTime(&ms, d.ev0, d.ev1);
     d.st.gpu_ms += ms;
     d.st.batches += 1;
+    if (d.shared_series != nullptr) d.st.shared_series_batches += 1;
     d.st.templates += nb;
     const uint32_t cnt = d.h_cands.p[0].x;
     if (cnt > d.cap) {

@@ -137,9 +137,12 @@ def test_app_binary_gpu(brp, gpu, case, tmp_path):
     assert lines[0][0] == pytest.approx(lc[0][0], rel=1e-9)
 
 
-def test_multi_wu_batching_matches_single_runs(brp, gpu, tmp_path):
-    """K same-shape WUs resident together, templates of different WUs mixed in
-    every batch: each WU's table equals its own single-WU run byte for byte."""
+@pytest.mark.parametrize("block_batches", [0, 1, 2])
+def test_multi_wu_batching_matches_single_runs(brp, gpu, tmp_path, block_batches):
+    """K same-shape WUs resident together, dealt WU-major in blocks of
+    block_batches batches (0 = default 64: one block holds the 21-template bank;
+    1 and 2 cross many block boundaries): each WU's table equals its own
+    single-WU run byte for byte."""
     from boinc_app_eah_brp_amd.models import MultiWUSearch
 
     wus = []
@@ -151,7 +154,7 @@ def test_multi_wu_batching_matches_single_runs(brp, gpu, tmp_path):
     cfg = SearchConfig(inputfile=wus[0]["wu"], templatebank=bank, zaplistfile=wus[0]["zap"], f0=400.0, padding=3.0,
                        fA=0.08, window=100, white=True, batch=4)
     ms = MultiWUSearch([c["wu"] for c in wus], cfg, pipelines=2)
-    tables = ms.step()
+    tables = ms.step(block_batches=block_batches)
     assert len(tables) == 3
     for k, c in enumerate(wus):
         single = BRPSearch(_cfg(c, tmp_path / f"s{k}", templatebank=bank, batch=4)).run(write_output=False,
@@ -332,5 +335,34 @@ def test_pipelines_sharing_one_series_equal_single_pipeline(brp, gpu, case, tmp_
     ctx = bd.DistContext(rank=0, world=1, local_rank=0, backend="none")
     one = bytes(bd.ShardedSearch(opts, ctx, device=0, streams=1).step().to_bytes())
     three = bd.ShardedSearch(opts, ctx, device=0, streams=3)
+    shared = []
     for _ in range(3):
         assert bytes(three.step().to_bytes()) == one
+        shared.append(three.session.stats()["shared_series_batches"])
+    # passes 2 and 3 really read pipeline 1's series in place (not a copy each)
+    assert shared[1] > shared[0] and shared[2] > shared[1], shared
+
+
+def test_stale_adopted_series_is_refused(brp, gpu, case):
+    """A pipeline that adopted another engine's series must not launch once the
+    source rewrote it (set up again for another WU) or was destroyed."""
+    hdr, series, _ = brp.read_work_unit(case["wu"])
+    geom = brp.derive_geometry(hdr, dict(f0=400.0, padding=3.0, fA=0.08, window=100))
+    src, rd = brp.HipEngine(), brp.HipEngine()
+    for e in (src, rd):
+        e.init(0, 1)
+        e.setup(geom, series, float(np.mean(series)))
+    P, tau, psi = brp.read_template_bank(case["bank"])
+    args = (P[:1].astype(np.float32), tau[:1].astype(np.float32), psi[:1].astype(np.float32), [30.0] * 5)
+    rd.adopt_series(src)
+    rd.process(*args)  # valid while the source is unchanged
+    src.setup(geom, series * 2.0, float(np.mean(series)) * 2.0)  # rewrites the adopted buffer
+    with pytest.raises(RuntimeError):
+        rd.process(*args)
+    rd.adopt_series(src)
+    rd.process(*args)
+    del src
+    import gc
+    gc.collect()
+    with pytest.raises(RuntimeError):
+        rd.process(*args)
