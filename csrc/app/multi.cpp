@@ -82,6 +82,7 @@ BackendStats MultiSession::stats() const {
     t.batches += s.batches;
     t.overflow_reruns += s.overflow_reruns;
     t.shared_series_batches += s.shared_series_batches;
+    t.peer_series_copies += s.peer_series_copies;
   }
   return t;
 }

@@ -168,6 +168,7 @@ BackendStats SearchSession::stats() const {
     t.batches += s.batches;
     t.overflow_reruns += s.overflow_reruns;
     t.shared_series_batches += s.shared_series_batches;
+    t.peer_series_copies += s.peer_series_copies;
   }
   return t;
 }
@@ -207,6 +208,12 @@ int SearchSession::open(const SearchOptions& opt, const SearchControl& ctl) {
   }
   // one backend per device; with the CPU golden model, one per worker thread
   int ngpu = std::max(1, ctl.gpus);
+  if (const char* rep = std::getenv("BRP_REPLAY_BACKEND")) {
+    // applier load test: ctl.gpus x ctl.pipelines no-compute backends
+    const int nb = ngpu * std::max(1, ctl.pipelines);
+    for (int k = 0; k < nb; ++k) d.backends.push_back(make_replay_backend(std::atoi(rep), std::max(1, opt.batch)));
+    return 0;
+  }
   if (!d.opt.use_cpu && !hip_backend_supports(d.g)) {
     // FFTW accepts any length; the HIP FFT is compiled for N/2 = L1*L2*L3 over
     // 16*2^a*3^b*5^c lengths. Other paddings run on the CPU golden model.
@@ -248,17 +255,29 @@ int SearchSession::prepare() {
   Impl& d = *impl_;
   trace::Range range("brp:prepare");
   boinc::begin_critical_section();
-  // the host copy of the whitened series only feeds backends that cannot take
-  // it device to device
-  bool adopt_all = true;
-  for (size_t k = 1; k < d.backends.size(); ++k) adopt_all = adopt_all && d.backends[k]->can_setup_from(*d.backends[0], d.g);
+  // every other backend takes the first one's whitened series device to
+  // device (same device: in place; other devices: peer copy from that
+  // device's first pipeline, which copied it from backend 0 over xGMI), so
+  // the host copy-back of the whitened series is only needed otherwise
+  const size_t nb = d.backends.size();
+  std::vector<size_t> src(nb, 0);
+  for (size_t k = 1; k < nb; ++k) {
+    const int dev = d.backends[k]->device();
+    for (size_t j = 0; j < k; ++j)
+      if (dev >= 0 && d.backends[j]->device() == dev) {
+        src[k] = j;
+        break;
+      }
+  }
+  bool device_all = true;
+  for (size_t k = 1; k < nb; ++k) device_all = device_all && d.backends[k]->can_setup_from(*d.backends[src[k]], d.g);
   SearchOptions opt0 = d.opt;
-  opt0.device_series = adopt_all;
+  opt0.device_series = device_all;
   const bool hip0 = std::strcmp(d.backends[0]->name(), "hip") == 0;
   if (hip0 && !d.wu_pin) d.wu_pin = hip_pin_host(d.wu.samples.data(), d.wu.samples.size() * sizeof(float));
   // a HIP backend that keeps the whitened series on the device only reads
   // the raw samples: upload them straight from the (page-locked) WU buffer
-  const bool direct = hip0 && adopt_all;
+  const bool direct = hip0 && device_all;
   if (!direct) d.series = d.wu.samples;
   int rc = d.backends[0]->setup(d.g, opt0, direct ? d.wu.samples : d.series, d.zaps);
   if (rc) {
@@ -268,13 +287,14 @@ int SearchSession::prepare() {
   SearchOptions opt_nw = d.opt;
   opt_nw.white = false;
   opt_nw.prewhitened = d.opt.white;
-  // the other backends take the whitened series (~11 ms each on MI355X;
-  // concurrent setups from several host threads measured no faster: the HIP
-  // runtime serialises the allocations and uploads)
-  for (size_t k = 1; k < d.backends.size(); ++k) {
-    // same device, same shape as last pass: device-to-device copy of the
-    // first backend's whitened series (no host round trip)
-    if (d.backends[k]->setup_from(*d.backends[0], d.g) == 0) continue;
+  for (size_t k = 1; k < nb; ++k) {
+    if (d.backends[k]->setup_from(*d.backends[src[k]], d.g) == 0) continue;
+    if (device_all) {
+      // the host never received the whitened series
+      log_message(LOG_ERROR, true, "Pipeline %zu could not take the whitened series from pipeline %zu.\n", k, src[k]);
+      boinc::end_critical_section();
+      return RADPUL_HIP_MEM_COPY_HOST_DEVICE;
+    }
     std::vector<float> s = d.series;
     rc = d.backends[k]->setup(d.g, opt_nw, s, d.zaps);
     if (rc) {
@@ -338,7 +358,7 @@ int SearchSession::run(uint32_t begin, uint32_t end, CandidateTable& table, Sear
   uint32_t applied = begin;
   int rc = 0;
   bool quit = false;
-  std::set<uint32_t> pages;
+  std::vector<uint32_t> pages;  // distinct dirty pages per level (statistics)
   SearchInfo& info = d.info;
   while (applied < end && !quit) {
     BatchResult br;
@@ -364,8 +384,9 @@ int SearchSession::run(uint32_t begin, uint32_t end, CandidateTable& table, Sear
         if (lv.empty()) continue;
         pages.clear();
         for (const BinPower& bp : lv)
-          if (bp.power > thrA[h]) pages.insert(bp.bin >> kLogPsPageSize);
-        res.dirty_pages += pages.size();
+          if (bp.power > thrA[h]) pages.push_back(bp.bin >> kLogPsPageSize);
+        std::sort(pages.begin(), pages.end());
+        res.dirty_pages += static_cast<uint64_t>(std::unique(pages.begin(), pages.end()) - pages.begin());
         if (h == 2) {
           const float powerscale = 100.0f / 255.0f;
           const float stepscale = static_cast<float>(kBinsScreensaver) / static_cast<float>(g.fundamental_idx_hi);

@@ -485,6 +485,7 @@ PYBIND11_MODULE(_brp, m) {
         d["batches"] = s.batches;
         d["overflow_reruns"] = s.overflow_reruns;
         d["shared_series_batches"] = s.shared_series_batches;
+        d["peer_series_copies"] = s.peer_series_copies;
         return d;
       });
   m.def("fft_plan", [](uint32_t M) -> py::object {
@@ -496,7 +497,8 @@ PYBIND11_MODULE(_brp, m) {
   // ---------------------------------------------------------------- driver
   m.def(
       "run_search",
-      [](const py::dict& od, uint32_t begin, uint32_t end, bool write_output, bool use_checkpoint, int gpus) {
+      [](const py::dict& od, uint32_t begin, uint32_t end, bool write_output, bool use_checkpoint, int gpus,
+         int pipelines, uint32_t progress_every) {
         SearchOptions opt = dict_to_options(od);
         SearchControl ctl;
         ctl.begin = begin;
@@ -504,6 +506,8 @@ PYBIND11_MODULE(_brp, m) {
         ctl.write_output = write_output;
         ctl.use_checkpoint = use_checkpoint;
         ctl.gpus = gpus;
+        ctl.pipelines = std::max(1, pipelines);
+        ctl.progress_every = std::max<uint32_t>(1, progress_every);
         SearchResult res;
         int rc;
         {
@@ -526,7 +530,7 @@ PYBIND11_MODULE(_brp, m) {
         return d;
       },
       py::arg("options"), py::arg("begin") = 0, py::arg("end") = 0, py::arg("write_output") = true,
-      py::arg("use_checkpoint") = true, py::arg("gpus") = 1);
+      py::arg("use_checkpoint") = true, py::arg("gpus") = 1, py::arg("pipelines") = 1, py::arg("progress_every") = 1);
   py::class_<SearchSession>(m, "SearchSession")
       .def(py::init<>())
       .def(
@@ -574,6 +578,7 @@ PYBIND11_MODULE(_brp, m) {
         d["batches"] = st.batches;
         d["overflow_reruns"] = st.overflow_reruns;
         d["shared_series_batches"] = st.shared_series_batches;
+        d["peer_series_copies"] = st.peer_series_copies;
         return d;
       });
   py::class_<MultiSession>(m, "MultiSession")

@@ -30,6 +30,7 @@ struct BackendStats {
   uint64_t batches = 0;
   uint64_t overflow_reruns = 0;
   uint64_t shared_series_batches = 0;  // batches that read another pipeline's series in place
+  uint64_t peer_series_copies = 0;     // series taken device to device (peer / D2D), not from the host
 };
 
 class Backend {
@@ -44,8 +45,9 @@ class Backend {
   // thresholds of every template in the batch).
   virtual int process(const TemplateInput* t, int n, const float thr[kNumHarmonicLevels],
                       std::vector<TemplateCands>& out) = 0;
-  // Same-device shortcut for the next pass: take `first`'s prepared (whitened)
-  // series without a host round trip. Nonzero: not applicable, use setup().
+  // Take `first`'s prepared (whitened) series without a host round trip (same
+  // device: read in place; another device: peer copy). can_setup_from() is
+  // decided before `first` is set up; setup_from() != 0: not applicable.
   virtual bool can_setup_from(const Backend& first, const SearchGeometry& g) const {
     (void)first;
     (void)g;
@@ -57,10 +59,13 @@ class Backend {
     return -1;
   }
   virtual int preferred_batch() const = 0;
+  virtual int device() const { return -1; }
   virtual BackendStats stats() const { return {}; }
 };
 
 std::unique_ptr<Backend> make_cpu_backend();
+// no-compute backend returning synthetic candidate lists (applier load tests)
+std::unique_ptr<Backend> make_replay_backend(int per_level, int batch);
 // device < 0: auto (BOINC gpu_device_num / first device)
 // True when the HIP pipeline has a compiled FFT plan for this geometry
 // (N even and N/2 = L1*L2*L3 over the compiled lengths, fft_passes.hip).

@@ -616,6 +616,36 @@ bool same_geometry(const SearchGeometry& a, const SearchGeometry& b) {
 }  // namespace
 
 int HipEngine::setup(const SearchGeometry& g, const std::vector<float>& series, float mu0) {
+  if (series.size() < g.n_unpadded) return RADPUL_EVAL;
+  return setup_impl(g, series.data(), nullptr, -1, mu0);
+}
+
+int HipEngine::setup_peer(const HipEngine& src) {
+  const Impl& s = *src.impl_;
+  if (!s.ready || s.slots != 1) return RADPUL_EVAL;
+  // the source's whitening ran on its own stream
+  BRP_HIP_CHECK(hipSetDevice(s.device), RADPUL_HIP_DEVICE_SET);
+  BRP_HIP_CHECK(hipStreamSynchronize(s.stream), RADPUL_HIP_MEM_COPY_HOST_DEVICE);
+  return setup_impl(s.g, nullptr, s.series_in(), s.device, s.mu0s[0]);
+}
+
+int HipEngine::upload_series0(const float* host, const float* dev_src, int src_device) {
+  Impl& d = *impl_;
+  const size_t bytes = d.g.n_unpadded * sizeof(float);
+  if (dev_src != nullptr) {
+    // device to device: same device, or a peer over xGMI (no host round trip)
+    trace::Range up("brp:series_peer_copy");
+    BRP_HIP_CHECK(hipMemcpyPeer(d.series.p, d.device, dev_src, src_device, bytes), RADPUL_HIP_MEM_COPY_HOST_DEVICE);
+    d.st.peer_series_copies += 1;
+    return 0;
+  }
+  trace::Range up("brp:series_upload");
+  BRP_HIP_CHECK(hipMemcpy(d.series.p, host, bytes, hipMemcpyHostToDevice), RADPUL_HIP_MEM_COPY_HOST_DEVICE);
+  return 0;
+}
+
+int HipEngine::setup_impl(const SearchGeometry& g, const float* host_series, const float* dev_series, int src_device,
+                          float mu0) {
   trace::Range range("brp:engine_setup");
   Impl& d = *impl_;
   BRP_HIP_CHECK(hipSetDevice(d.device), RADPUL_HIP_DEVICE_SET);
@@ -626,10 +656,7 @@ int HipEngine::setup(const SearchGeometry& g, const std::vector<float>& series, 
     d.g = g;
     d.mu0s.assign(d.slots, 0.0f);
     d.mu0s[0] = mu0;
-    trace::Range up("brp:series_upload");
-    BRP_HIP_CHECK(hipMemcpy(d.series.p, series.data(), g.n_unpadded * sizeof(float), hipMemcpyHostToDevice),
-                  RADPUL_HIP_MEM_COPY_HOST_DEVICE);
-    return 0;
+    return upload_series0(host_series, dev_series, src_device);
   }
   d.ready = false;
   for (auto& kv : d.graphs) (void)hipGraphExecDestroy(kv.second);
@@ -743,8 +770,7 @@ int HipEngine::setup(const SearchGeometry& g, const std::vector<float>& series, 
   BRP_HIP_CHECK(hipMemcpy(d.tw_lo.p, lo.data(), lo.size() * sizeof(float2), hipMemcpyHostToDevice),
                 RADPUL_HIP_MEM_COPY_HOST_DEVICE);
   if ((rc = d.build_tables())) return rc;
-  BRP_HIP_CHECK(hipMemcpy(d.series.p, series.data(), g.n_unpadded * sizeof(float), hipMemcpyHostToDevice),
-                RADPUL_HIP_MEM_COPY_HOST_DEVICE);
+  if ((rc = upload_series0(host_series, dev_series, src_device))) return rc;
   log_mem_status(d.device, "after setup");
   d.ready = true;
   return 0;
@@ -1266,15 +1292,28 @@ class HipBackend final : public Backend {
               std::vector<TemplateCands>& out) override {
     return eng_.process(t, n, thr, out);
   }
+  // any HIP backend can take the first
+  // backend's whitened series without a host round trip: pipelines on the same
+  // device read it in place (adopt_series), other devices get a peer copy over
+  // xGMI (setup_peer). BRP_PEER_SERIES=1 forces the copy on one device (tests).
   bool can_setup_from(const Backend& first, const SearchGeometry& g) const override {
+    (void)g;
     const auto* src = dynamic_cast<const HipBackend*>(&first);
-    return src != nullptr && src != this && eng_.ps_fp16() == src->eng_.ps_fp16() && eng_.device() == src->eng_.device() &&
-           eng_.prepared_for(g) && src->eng_.prepared_for(g);
+    return src != nullptr && src != this;
   }
   int setup_from(const Backend& first, const SearchGeometry& g) override {
     if (!can_setup_from(first, g)) return -1;
-    return eng_.adopt_series(dynamic_cast<const HipBackend&>(first).eng_) == 0 ? 0 : -1;
+    const HipEngine& src = dynamic_cast<const HipBackend&>(first).eng_;
+    if (!src.prepared_for(g)) return -1;
+    eng_.set_ps_fp16(src.ps_fp16());  // the session's spectrum precision
+    const bool force_peer = std::getenv("BRP_PEER_SERIES") != nullptr && std::atoi(std::getenv("BRP_PEER_SERIES")) != 0;
+    if (eng_.device() == src.device() && !force_peer) {
+      if (!eng_.prepared_for(g) && eng_.setup_peer(src) != 0) return -1;  // first pass: allocate (D2D copy)
+      return eng_.adopt_series(src) == 0 ? 0 : -1;
+    }
+    return eng_.setup_peer(src) == 0 ? 0 : -1;
   }
+  int device() const override { return eng_.device(); }
   int preferred_batch() const override { return eng_.batch(); }
   BackendStats stats() const override { return eng_.stats(); }
 

@@ -29,6 +29,10 @@ class HipEngine {
   // copies it device to device with BRP_SHARE_SERIES=0. setup(), load_slot()
   // and whiten() return to the engine's own buffer. RADPUL_EVAL when not applicable.
   int adopt_series(const HipEngine& src);
+  // Set up from `src`'s prepared (whitened) series, device to device: a
+  // hipMemcpyPeer over xGMI when `src` is on another device, a D2D copy on the
+  // same one. Allocates like setup() on first use. No host round trip.
+  int setup_peer(const HipEngine& src);
   // Multi-WU batching: the series buffer holds `k` work units of the same
   // shape (set before setup(); setup() fills slot 0, load_slot() the others).
   // Templates pick their slot with TemplateInput::wu.
@@ -60,6 +64,9 @@ class HipEngine {
   const FFTPlan3& plan() const;
 
  private:
+  int setup_impl(const SearchGeometry& g, const float* host_series, const float* dev_series, int src_device,
+                 float mu0);
+  int upload_series0(const float* host, const float* dev_src, int src_device);
   struct Impl;
   Impl* impl_;
 };

@@ -343,6 +343,26 @@ def test_pipelines_sharing_one_series_equal_single_pipeline(brp, gpu, case, tmp_
     assert shared[1] > shared[0] and shared[2] > shared[1], shared
 
 
+def test_peer_series_copy_equals_single_pipeline(brp, gpu, case, tmp_path, monkeypatch):
+    """Pipelines on other devices take the whitened series by hipMemcpyPeer
+    (no host round trip). One box has one GPU, so BRP_PEER_SERIES=1 forces that
+    path between pipelines of device 0: same table as one pipeline, copies
+    counted, nothing read in place."""
+    from boinc_app_eah_brp_amd.parallel import dist as bd
+
+    monkeypatch.setenv("BRP_PEER_SERIES", "1")
+    opts = dict(inputfile=case["wu"], templatebank=case["bank"], zaplistfile=case["zap"], f0=400.0, padding=3.0,
+                fA=0.08, window=100, white=True, batch=1, outputfile=str(tmp_path / "x.cand"))
+    ctx = bd.DistContext(rank=0, world=1, local_rank=0, backend="none")
+    one = bytes(bd.ShardedSearch(opts, ctx, device=0, streams=1).step().to_bytes())
+    three = bd.ShardedSearch(opts, ctx, device=0, streams=3)
+    for step in range(2):
+        assert bytes(three.step().to_bytes()) == one
+        st = three.session.stats()
+        assert st["peer_series_copies"] == 2 * (step + 1), st
+        assert st["shared_series_batches"] == 0, st
+
+
 def test_stale_adopted_series_is_refused(brp, gpu, case):
     """A pipeline that adopted another engine's series must not launch once the
     source rewrote it (set up again for another WU) or was destroyed."""
