@@ -238,6 +238,60 @@ class ShardedSearch:
             self.timings[k] = self.timings.get(k, 0.0) + v
         return merged
 
+    def search(self, chunk: int = 2048, kill_after: int | None = None, on_chunk=None):
+        """The whole work unit with the application's checkpoint semantics.
+
+        The bank is cut into chunks of `chunk` templates; every rank searches
+        its shard_range of the chunk, the tables are all-gathered and merged
+        into the running table in template order, so after each chunk the
+        merged table covers exactly the prefix [0, n). Rank 0
+        then writes the reference-format checkpoint (n, table) atomically.
+        A restart reads it on every rank (same node, same file) and resumes at
+        n; the result file is written by rank 0 at the end. `kill_after`
+        stops (like a BOINC quit: no final checkpoint, no result) after the
+        chunk that reaches that many templates. Returns (table, n_done)."""
+        brp = self.brp
+        cp = self.options.get("checkpointfile") or ""
+        table = brp.CandidateTable()
+        n = 0
+        if cp and os.path.exists(cp):
+            got = brp.read_checkpoint(cp)
+            if got is not None:
+                n_cp, orig, t = got
+                if orig != self.options["inputfile"]:
+                    raise RuntimeError(f"checkpoint {cp} belongs to {orig}, not {self.options['inputfile']}")
+                if n_cp > self.total:
+                    raise RuntimeError(f"checkpoint {cp}: {n_cp} templates done > bank size {self.total}")
+                n, table = int(n_cp), t
+        t0 = time.perf_counter()
+        self.session.prepare()
+        t1 = time.perf_counter()
+        search_s = 0.0
+        while n < self.total:
+            hi = min(self.total, n + max(1, chunk))
+
+            def run_shard(begin, end, lo=n):
+                nonlocal search_s
+                ts = time.perf_counter()
+                t, _ = self.session.run(lo + begin, lo + end, brp.CandidateTable())
+                search_s += time.perf_counter() - ts
+                return [t]
+
+            part = sharded_merge(run_shard, hi - n, self.ctx)[0]
+            table.merge(part)
+            n = hi
+            if cp and self.ctx.rank == 0:
+                brp.write_checkpoint(cp, n, self.options["inputfile"], table)
+            if on_chunk is not None:
+                on_chunk(n, self.total)
+            if kill_after is not None and n >= kill_after and n < self.total:
+                return table, n
+        t2 = time.perf_counter()
+        for k, v in (("prepare", t1 - t0), ("templates", search_s), ("merge", t2 - t1 - search_s)):
+            self.timings[k] = self.timings.get(k, 0.0) + v
+        self.write_output(table, n)
+        return table, n
+
     def write_output(self, table, n_done: int | None = None):
         """Rank 0 writes the checkpoint/result files of the merged table."""
         if self.ctx.rank != 0:

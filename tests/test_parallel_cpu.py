@@ -62,3 +62,51 @@ def test_gloo_sharded_equals_single(brp, tmp_path):
     # identical result files (ignoring the optional comment header)
     strip = lambda p: [l for l in open(p).read().splitlines() if not l.startswith("% ")]
     assert strip(tmp_path / "dist.cand") == strip(tmp_path / "single.cand")
+
+
+def _cp_worker(rank, world, port, opts, out_dir, kill_after):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    ctx = pdist.init_distributed("gloo")
+    try:
+        ss = pdist.ShardedSearch(opts, ctx, use_cpu=True)
+        table, n = ss.search(chunk=7, kill_after=kill_after)
+        if rank == 0:
+            np.save(os.path.join(out_dir, f"n_{kill_after}.npy"), np.array([n]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_chunked_checkpoint_resume_equals_single(brp, tmp_path):
+    """torchrun path with the app's checkpoint semantics: chunks of 7 templates
+    all-gathered and merged in order, rank 0 checkpoints the prefix after each
+    chunk; a run stopped after 14 templates resumes from the checkpoint on a new
+    process group and writes the single-process result file byte for byte."""
+    import torch.multiprocessing as mp
+
+    inj = synth.Injection(f0=173.0, P_orb=1200.0, tau=0.05, psi0=2.0, amplitude=3.0)
+    case = synth.synthetic_case(tmp_path / "case", n=1 << 14, n_templates=29, inj=inj)
+    opts = dict(inputfile=case["wu"], templatebank=case["bank"], zaplistfile=case["zap"],
+                outputfile=str(tmp_path / "dist.cand"), checkpointfile=str(tmp_path / "dist.cpt"), f0=400.0,
+                padding=3.0, fA=0.08, window=100, white=True, batch=2, use_cpu=True)
+    os.environ["BRP_NO_RESULT_HEADER"] = "1"
+    try:
+        mp.start_processes(_cp_worker, args=(2, _free_port(), opts, str(tmp_path), 14), nprocs=2, join=True,
+                           start_method="spawn")
+        assert int(np.load(tmp_path / "n_14.npy")[0]) == 14
+        assert not os.path.exists(opts["outputfile"])
+        n_cp, orig, _ = brp.read_checkpoint(opts["checkpointfile"])
+        assert n_cp == 14 and orig == case["wu"]
+        mp.start_processes(_cp_worker, args=(2, _free_port(), opts, str(tmp_path), None), nprocs=2, join=True,
+                           start_method="spawn")
+        assert int(np.load(tmp_path / "n_None.npy")[0]) == 30
+        single = dict(opts, outputfile=str(tmp_path / "single.cand"), checkpointfile=str(tmp_path / "single.cpt"))
+        r = brp.run_search(single, 0, 0, True, False)
+        assert r["templates_run"] == 30
+    finally:
+        del os.environ["BRP_NO_RESULT_HEADER"]
+    assert open(opts["outputfile"]).read() == open(single["outputfile"]).read()
+    n_cp, _, _ = brp.read_checkpoint(opts["checkpointfile"])
+    assert n_cp == 30
