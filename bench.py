@@ -52,6 +52,9 @@ def parse():
                     help="work units resident per GPU (config 4): the reference WU + synthetic WUs of its shape")
     ap.add_argument("--synthetic", action="store_true", help="synthetic WU/bank of the benchmark shape")
     ap.add_argument("--write-output", default="", help="rank 0 writes the result file of the last step here")
+    ap.add_argument("--shard-of", default="",
+                    help="N:R = time only rank R's template block of an N-rank run on this one GPU "
+                         "(compute-only scaling proxy; no collectives; not the driver's metric)")
     ap.add_argument("--cpu", action="store_true",
                     help="rehearsal of the multi-rank path without GPUs: gloo collectives, CPU golden backend, "
                          "small synthetic WU (not a benchmark; used by tests/test_bench_cpu.py)")
@@ -126,8 +129,13 @@ def main() -> int:
     from boinc_app_eah_brp_amd.parallel import ShardedSearch, barrier, init_distributed, max_over_ranks
 
     ctx = init_distributed("gloo" if args.cpu else None)
+    if args.shard_of:
+        from boinc_app_eah_brp_amd.parallel import DistContext
+
+        n_of, r_of = (int(x) for x in args.shard_of.split(":"))
+        ctx = DistContext(rank=r_of, world=n_of, local_rank=ctx.local_rank, backend="none", solo_shard=True)
     use_gpu = torch.cuda.is_available() and not args.cpu
-    world = ctx.world
+    world = 1 if ctx.solo_shard else ctx.world
     if world != args.gpus and ctx.rank == 0:
         print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}", file=sys.stderr)
     brp = native()
@@ -170,9 +178,11 @@ def main() -> int:
     if use_gpu:
         torch.cuda.synchronize()
 
+    lead = ctx.rank == 0 or ctx.solo_shard
+
     def progress(msg):
         # long runs (config 4 at many WUs) stay visibly alive on stderr; stdout keeps the one JSON line
-        if ctx.rank == 0:
+        if lead:
             print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
     table = None
@@ -198,12 +208,18 @@ def main() -> int:
     if args.write_output and n_wus == 1:
         search.write_output(table, limit)
     stats = search.session.stats()
-    if ctx.rank == 0:
+    if lead:
         geom = search.session.geometry()
-        total = limit * args.steps * n_wus
+        work = limit
+        if ctx.solo_shard:
+            from boinc_app_eah_brp_amd.parallel import shard_range
+
+            lo, hi = shard_range(limit, ctx.rank, ctx.world)
+            work = hi - lo
+        total = work * args.steps * n_wus
         value = total / elapsed
         n_cands = sum(1 for e in table.entries() if e[5] > 0)
-        rec = recall_vs_golden(table, geom) if limit == search.total and not args.cpu else None
+        rec = recall_vs_golden(table, geom) if limit == search.total and not args.cpu and not ctx.solo_shard else None
         out = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -238,6 +254,9 @@ def main() -> int:
                 "work_units": n_wus,
             },
         }
+        if ctx.solo_shard:
+            out["shard_of"] = {"world": ctx.world, "rank": ctx.rank, "templates": work,
+                               "note": "compute-only timing of one rank's block on one GPU (no collectives)"}
         print(json.dumps(out), flush=True)
     if ctx.distributed:
         import torch.distributed as dist

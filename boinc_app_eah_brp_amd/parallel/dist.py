@@ -44,10 +44,11 @@ class DistContext:
     device: object = None  # torch.device of the collectives
     degraded: bool = False  # a collective failed: this rank now searches alone
     stalled: bool = False   # the collective_timeout fault already fired
+    solo_shard: bool = False  # one process times rank `rank`'s shard of a `world`-rank run (no collectives)
 
     @property
     def distributed(self) -> bool:
-        return self.world > 1 and not self.degraded
+        return self.world > 1 and not self.degraded and not self.solo_shard
 
 
 class CollectiveError(RuntimeError):
@@ -158,6 +159,8 @@ def sharded_merge(run_shard, total: int, ctx: DistContext) -> list:
     run_shard(begin, end) returns one candidate table per work unit. If the
     all-gather fails the rank degrades (see `degrade`) and runs the missing
     shards itself, so the merged tables are the same either way."""
+    if ctx.solo_shard:
+        return run_shard(*shard_range(total, ctx.rank, ctx.world))
     if not ctx.distributed:
         return run_shard(0, total)
     shards = [shard_range(total, r, ctx.world) for r in range(ctx.world)]

@@ -362,9 +362,6 @@ PYBIND11_MODULE(_brp, m) {
     py::dict d;
     d["found"] = w.found;
     d["persist_per_cu"] = w.persist_per_cu;
-    d["fft_passes"] = w.fft_passes;
-    d["hs_stage"] = w.hs_stage;
-    d["hs_tile"] = w.hs_tile;
     d["batch"] = w.batch;
     d["pipelines"] = w.pipelines;
     return d;

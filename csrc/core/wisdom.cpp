@@ -78,9 +78,6 @@ PlanWisdom load_wisdom(const std::string& path, const std::string& arch, uint32_
     if (field(obj, "arch", ea) && arch_base(ea) == arch_base(arch) && int_field(obj, "M") == static_cast<int>(M)) {
       w.found = true;
       w.persist_per_cu = int_field(obj, "persist_per_cu");
-      w.fft_passes = int_field(obj, "fft_passes");
-      w.hs_stage = int_field(obj, "hs_stage");
-      w.hs_tile = int_field(obj, "hs_tile");
       w.batch = int_field(obj, "batch");
       w.pipelines = int_field(obj, "pipelines");
       return w;

@@ -2,12 +2,10 @@
 // counterpart of the reference's FFTW wisdom (demod_binary_fft_fftw.c:65-69,
 // debian/extra/create_wisdomf_eah_brp.sh). tools/tune_plan.py measures the
 // candidates on the target GPU and writes data/wisdom/mi355x.json; the HIP
-// engine applies the entry of its (arch, M) at setup. Environment variables
-// (BRP_PERSIST, BRP_FFT2, BRP_HS_STAGE, BRP_HS_TILE) override it.
+// engine applies the entry of its (arch, M) at setup; BRP_PERSIST overrides it.
 //
 // Format (JSON): {"entries": [{"arch": "gfx950", "M": 6291456,
-//                  "persist_per_cu": 4, "fft_passes": 3, "hs_stage": 0, "hs_tile": 1008,
-//                  "batch": 1, "pipelines": 3, ...}, ...]}
+//                  "persist_per_cu": 4, "batch": 1, "pipelines": 3, ...}, ...]}
 #pragma once
 
 #include <cstdint>
@@ -18,9 +16,6 @@ namespace brp {
 struct PlanWisdom {
   bool found = false;
   int persist_per_cu = -1;  // pass-2 persistent workgroups per CU
-  int fft_passes = -1;      // 3 or 2 (two-pass template FFT)
-  int hs_stage = -1;        // harmonics staged in LDS by the harmonic sum
-  int hs_tile = -1;         // harmonic-sum bins per workgroup
   int batch = -1;           // templates per device batch
   int pipelines = -1;       // pipelines per GPU
 };

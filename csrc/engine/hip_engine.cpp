@@ -27,7 +27,6 @@
 #include "../core/log.hpp"
 #include "../core/rngmed.hpp"
 #include "../core/wisdom.hpp"
-#include "../hip/fft2_kernels.hpp"
 #include "../hip/fft_kernels.hpp"
 #include "../hip/hs_kernels.hpp"
 #include "../hip/resample_kernels.hpp"
@@ -204,20 +203,9 @@ struct HipEngine::Impl {
   uint32_t num_cus = 256;
   std::string arch;             // gcnArchName (plan-wisdom lookup)
   bool ps_fp16 = false;         // config 5: fp16 power spectrum between pass 3 and the harmonic sum
-  // harmonic-sum variant: harmonics 1..n staged in LDS, the rest gathered (BRP_HS_STAGE)
-  int hs_stage = 0;
-  uint32_t hs_xcd = 0;          // BRP_HS_XCD=1: XCD-contiguous harmonic-sum tiles
-  uint32_t hs_tile = 0;         // harmonic-sum bins per workgroup (wisdom / BRP_HS_TILE, 0 = kHsTile)
-  // harmonic-sum kernel: per-i gathers (default), or the measured-equal /
-  // slower register-blocked layouts (BRP_HS_KERNEL=quad / rb, fp32 spectrum only)
-  int hs_variant = hipk::HS_GATHER;
-  int hs_rb_occ = 0;
   uint32_t persist_per_cu = 4;  // persistent FFT passes: workgroups per CU (BRP_PERSIST, 0 = off)
   uint32_t ps_stride = 0;
-  uint32_t i_start = 0;
-  // two-pass template FFT (fft2.hip) for the 3x-padded production shape
-  // M = 768 * 8192; the three-pass plan stays in use for whitening
-  bool two_pass = false;
+  int32_t i_start = 0;
   // per-batch parameters / candidate results in fine-grained device memory the
   // host writes / reads directly, instead of two small copies per batch
   // (each a runtime blit kernel on the GPU); BRP_FG=in|out|both|0
@@ -264,8 +252,6 @@ struct HipEngine::Impl {
   DevBuf<uint32_t> w_zbins;     // whitening: zapped bins and their noise
   DevBuf<float2> w_znoise;
   DevBuf<float2> t_st1, t_st2, t_st3, t_p1, t_p2col, t_p2lo, t_p2hi, t_p3;
-  DevBuf<float2> t_w768, t_t256, t_t4096, t_t8192;  // two-pass tables
-  DevBuf<float> pss;            // [batch][M] slab-major power spectrum (two-pass)
 
   PinnedBuf<uint8_t> h_in;
   struct { TemplateDev* p = nullptr; } h_tmpl;
@@ -326,22 +312,6 @@ struct HipEngine::Impl {
     for (uint32_t i = 0; i < 32; ++i) v[i] = root(i, 4ull * L3);
     for (uint32_t m = 0; m < 4 * L3 / 32; ++m) v[32 + m] = root(32ull * m, 4ull * L3);
     if ((rc = upload(t_p3, v))) return rc;
-    if (!two_pass) return 0;
-    v.assign(hipk::kFft2L1, make_float2(0, 0));
-    for (uint32_t e = 0; e < hipk::kFft2L1; ++e) v[e] = root(e, hipk::kFft2L1);
-    if ((rc = upload(t_w768, v))) return rc;
-    v.assign(256, make_float2(0, 0));
-    for (uint32_t e = 0; e < 256; ++e) v[e] = root(e, 256);
-    if ((rc = upload(t_t256, v))) return rc;
-    // two-level W_4096 / W_8192: lo[e & 63] * hi[e >> 6]
-    for (uint32_t n : {4096u, 8192u}) {
-      v.assign(128, make_float2(0, 0));
-      for (uint32_t e = 0; e < 64; ++e) {
-        v[e] = root(e, n);
-        v[64 + e] = root(64ull * e, n);
-      }
-      if ((rc = upload(n == 4096 ? t_t4096 : t_t8192, v))) return rc;
-    }
     return 0;
   }
 
@@ -374,19 +344,6 @@ struct HipEngine::Impl {
         if (fg_in) return hipSuccess;  // the host wrote `in` directly
         return hipMemcpyAsync(in.p, h_in.p, thr_bytes + sizeof(TemplateDev) * nb, hipMemcpyHostToDevice, stream);
       case kPass1: {
-        if (two_pass) {
-          hipk::ColAArgs aa{};
-          aa.out = buf.p;
-          aa.M = plan.M;
-          aa.series = series_in();
-          aa.n_unpadded = g.n_unpadded;
-          aa.tmpl = tmpl.p;
-          aa.partials = partials.p;
-          aa.tw = tw;
-          aa.w768 = t_w768.p;
-          aa.reset = &cands.p[0].x;
-          return hipk::launch_colA(aa, nb, stream);
-        }
         hipk::Pass1Args a1{};
         a1.out = buf.p;
         a1.L2L3 = plan.L2 * plan.L3;
@@ -401,26 +358,6 @@ struct HipEngine::Impl {
         return hipk::launch_pass1(plan, hipk::P1_RESAMPLE, a1, nb, stream);
       }
       case kPass2: {
-        if (two_pass) {
-          hipk::RowBArgs ab{};
-          ab.buf = buf.p;
-          ab.M = plan.M;
-          ab.tw = tw;
-          ab.t256 = t_t256.p;
-          ab.t4096 = t_t4096.p;
-          ab.t8192 = t_t8192.p;
-          ab.limit = std::min(g.harmonic_idx_hi, g.fft_size);
-          ab.pss = pss.p;
-          ab.pss_stride = plan.M;
-          ab.norm = static_cast<float>(1.0 / g.nsamples);
-          ab.tmpl = tmpl.p;
-          ab.partials = partials.p;
-          ab.n_partials = hipk::kFft2R / 16;
-          ab.ps = ps.p;
-          ab.ps16 = ps_fp16 ? reinterpret_cast<_Float16*>(ps.p) : nullptr;
-          ab.ps_stride = ps_stride;
-          return hipk::launch_rowB(ab, nb, stream);
-        }
         hipk::Pass2Args a2{};
         a2.buf = buf.p;
         a2.L1 = plan.L1;
@@ -435,17 +372,6 @@ struct HipEngine::Impl {
         return hipk::launch_pass2(plan, a2, nb, stream);
       }
       case kPass3: {
-        if (two_pass) {
-          hipk::PsTArgs at{};
-          at.pss = pss.p;
-          at.pss_stride = plan.M;
-          at.ps = ps.p;
-          at.ps16 = ps_fp16 ? reinterpret_cast<_Float16*>(ps.p) : nullptr;
-          at.ps_stride = ps_stride;
-          at.limit = std::min(g.harmonic_idx_hi, g.fft_size);
-          at.M = plan.M;
-          return hipk::launch_psT(at, nb, stream);
-        }
         hipk::Pass3Args a3{};
         a3.buf = buf.p;
         a3.L1 = plan.L1;
@@ -476,11 +402,6 @@ struct HipEngine::Impl {
         ah.thr = thr.p;
         ah.list = cands.p;
         ah.cap = cap;
-        ah.staged_harmonics = hs_stage;
-        ah.tile = hs_tile;
-        ah.xcd = hs_xcd;
-        ah.variant = ps_fp16 ? hipk::HS_GATHER : hs_variant;
-        ah.rb_occupancy = hs_rb_occ;
         return hipk::launch_harmonic_sum(ah, nb, stream);
       }
       case kEpilogue:
@@ -672,50 +593,23 @@ int HipEngine::setup_impl(const SearchGeometry& g, const float* host_series, con
   // measured settings for this (arch, M) from the plan wisdom; environment wins
   const PlanWisdom wis = load_wisdom(wisdom_path(), d.arch, d.plan.M);
   if (wis.found)
-    log_message(LOG_DEBUG, true, "Plan wisdom for %s M=%u: persist %d, FFT passes %d, HS stage %d, HS tile %d\n",
-                d.arch.c_str(), d.plan.M, wis.persist_per_cu, wis.fft_passes, wis.hs_stage, wis.hs_tile);
+    log_message(LOG_DEBUG, true, "Plan wisdom for %s M=%u: persist %d\n", d.arch.c_str(), d.plan.M,
+                wis.persist_per_cu);
   if (wis.persist_per_cu >= 0) d.persist_per_cu = static_cast<uint32_t>(wis.persist_per_cu);
   if (const char* e = std::getenv("BRP_PERSIST")) d.persist_per_cu = static_cast<uint32_t>(std::atoi(e));
-  d.hs_stage = wis.hs_stage >= 0 ? wis.hs_stage : 0;
-  if (const char* e = std::getenv("BRP_HS_STAGE")) d.hs_stage = std::atoi(e);
-  // 1008 bins per workgroup: the tile plus its 4-bin halo fit in 4 x 256
-  // lanes (1024 leaves a fifth pass of 4 lanes), +1.4% templates/s
-  d.hs_tile = wis.hs_tile > 0 ? static_cast<uint32_t>(wis.hs_tile) : 1008u;
-  if (const char* e = std::getenv("BRP_HS_TILE")) d.hs_tile = static_cast<uint32_t>(std::atoi(e));
-  if (const char* e = std::getenv("BRP_HS_XCD")) d.hs_xcd = static_cast<uint32_t>(std::atoi(e));
-  if (d.hs_stage != 0) d.hs_tile = hipk::kHsTile;  // the LDS staging layout is built for the default tile
-  d.hs_variant = hipk::HS_GATHER;
-  if (const char* e = std::getenv("BRP_HS_KERNEL"))
-    d.hs_variant = std::strcmp(e, "rb") == 0 ? hipk::HS_REGISTER_BLOCKED
-                   : std::strcmp(e, "quad") == 0 ? hipk::HS_QUAD
-                                                 : hipk::HS_GATHER;
-  if (d.hs_stage != 0 || d.hs_xcd != 0) d.hs_variant = hipk::HS_GATHER;
-  if (const char* e = std::getenv("BRP_HS_RB_OCC")) d.hs_rb_occ = std::atoi(e);
   d.plan.persist_wgs = d.persist_per_cu * d.num_cus;
-  // opt-in (BRP_FFT2=1): measured 84 vs 78 us/template sequential, the
-  // three-pass kernels keep more workgroups per CU (profiles/README.md)
-  const bool want2 = std::getenv("BRP_FFT2") ? std::atoi(std::getenv("BRP_FFT2")) != 0 : wis.fft_passes == 2;
-  d.two_pass = d.plan.M == hipk::kFft2M && 2ull * (hipk::kFft2L1 / 3) * hipk::kFft2R >= g.n_unpadded && want2;
-  d.plan.legacy_pass1 = std::getenv("BRP_P1_LEGACY") != nullptr;
-  d.plan.legacy_pass2 = std::getenv("BRP_P2_LEGACY") != nullptr;
   log_message(LOG_DEBUG, true, "FFT plan: N=%u M=%u = %u x %u x %u\n", g.nsamples, d.plan.M, d.plan.L1, d.plan.L2,
               d.plan.L3);
   const uint32_t limit = std::min(g.harmonic_idx_hi, g.fft_size);
   d.ps_stride = std::max<uint32_t>((std::max(limit, g.fundamental_idx_hi) + 63) / 64 * 64, 64);
-  d.i_start = (g.window_2 >= 8) ? ((g.window_2 - 8) / 16) * 16 + 8 : 8;
-  if (d.i_start > g.window_2) d.i_start = 8;  // unreachable; keeps the invariant i_start <= w2 for w2 >= 8
+  // first harmonic-sum tile: i_start == 8 mod 16 and <= window_2 (-8 below 8)
+  d.i_start = (g.window_2 >= 8) ? static_cast<int32_t>(((g.window_2 - 8) / 16) * 16 + 8) : -8;
   int rc;
   const size_t B = static_cast<size_t>(d.batch);
   if ((rc = d.series.alloc(static_cast<size_t>(d.slots) * g.n_unpadded))) return rc;
   if ((rc = d.buf.alloc(B * d.plan.M))) return rc;
-  // + slack: the harmonic-sum staging copies whole 64-float chunks past the last bin
-  if ((rc = d.ps.alloc(B * d.ps_stride + 1024))) return rc;
-  if ((rc = d.partials.alloc(B * std::max<size_t>(d.plan.wg1(), hipk::kFft2R / 16)))) return rc;
-  if (d.two_pass) {
-    if ((rc = d.pss.alloc(B * d.plan.M))) return rc;
-  } else {
-    d.pss.release();
-  }
+  if ((rc = d.ps.alloc(B * d.ps_stride))) return rc;
+  if ((rc = d.partials.alloc(B * d.plan.wg1()))) return rc;
   if ((rc = d.delta.alloc(B))) return rc;
   if (B > hipk::kHsMaxBatch || g.fundamental_idx_hi >= (1u << hipk::kHsBinBits)) {
     log_message(LOG_ERROR, true, "Batch %zu / fundamental_idx_hi %u beyond the candidate key packing.\n", B,
@@ -1113,53 +1007,6 @@ int HipEngine::power_spectrum(const TemplateInput& t, std::vector<float>& ps_out
                   RADPUL_HIP_MEM_COPY_HOST_DEVICE);
   std::atomic_thread_fence(std::memory_order_seq_cst);
   const hipk::TwiddleTable tw = d.twt();
-  if (d.two_pass) {
-    // the template pipeline's transform: pass A, pass B, transpose (all bins)
-    DevBuf<float> full;
-    int rc;
-    if ((rc = full.alloc(g.fft_size))) return rc;
-    hipk::ColAArgs aa{};
-    aa.out = d.buf.p;
-    aa.M = d.plan.M;
-    aa.series = d.series_in();
-    aa.n_unpadded = g.n_unpadded;
-    aa.tmpl = d.tmpl.p;
-    aa.partials = d.partials.p;
-    aa.tw = tw;
-    aa.w768 = d.t_w768.p;
-    BRP_HIP_CHECK(hipk::launch_colA(aa, 1, s), RADPUL_HIP_KERNEL_INVOKE);
-    hipk::RowBArgs ab{};
-    ab.buf = d.buf.p;
-    ab.M = d.plan.M;
-    ab.tw = tw;
-    ab.t256 = d.t_t256.p;
-    ab.t4096 = d.t_t4096.p;
-    ab.t8192 = d.t_t8192.p;
-    ab.limit = g.fft_size;
-    ab.pss = d.pss.p;
-    ab.pss_stride = d.plan.M;
-    ab.norm = static_cast<float>(1.0 / g.nsamples);
-    ab.tmpl = d.tmpl.p;
-    ab.partials = d.partials.p;
-    ab.n_partials = hipk::kFft2R / 16;
-    ab.ps = full.p;
-    ab.ps_stride = g.fft_size;
-    BRP_HIP_CHECK(hipk::launch_rowB(ab, 1, s), RADPUL_HIP_KERNEL_INVOKE);
-    hipk::PsTArgs at{};
-    at.pss = d.pss.p;
-    at.pss_stride = d.plan.M;
-    at.ps = full.p;
-    at.ps_stride = g.fft_size;
-    at.limit = g.fft_size;
-    at.M = d.plan.M;
-    BRP_HIP_CHECK(hipk::launch_psT(at, 1, s), RADPUL_HIP_KERNEL_INVOKE);
-    ps_out.resize(g.fft_size);
-    BRP_HIP_CHECK(hipMemcpyAsync(ps_out.data(), full.p, g.fft_size * sizeof(float), hipMemcpyDeviceToHost, s),
-                  RADPUL_HIP_MEM_COPY_DEVICE_HOST);
-    BRP_HIP_CHECK(hipStreamSynchronize(s), RADPUL_HIP_KERNEL_INVOKE);
-    if (n_steps) *n_steps = d.h_tmpl.p[0].n_steps;
-    return 0;
-  }
   hipk::Pass1Args a1{};
   a1.out = d.buf.p;
   a1.L2L3 = d.plan.L2 * d.plan.L3;

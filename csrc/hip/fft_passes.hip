@@ -708,7 +708,7 @@ bool pass3_length_supported(uint32_t L) {
 hipError_t launch_pass1(const FFTPlan3& plan, Pass1Mode mode, const Pass1Args& a, int batch, hipStream_t s) {
   const dim3 grid(plan.wg1(), batch);
   // padding >= 3x: every template's rows n1 >= L1/3 are zero (n_steps <= n_unpadded)
-  const bool pad3 = mode == P1_RESAMPLE && !plan.legacy_pass1 && plan.L1 % 3 == 0 &&
+  const bool pad3 = mode == P1_RESAMPLE && plan.L1 % 3 == 0 &&
                     2ull * (plan.L1 / 3) * a.L2L3 >= a.n_unpadded;
   if (pad3 && plan.L1 == 192) {
     hipLaunchKernelGGL((pass1_pruned3_kernel<4>), grid, dim3(kNcol * 16), 0, s, a);
@@ -737,16 +737,16 @@ hipError_t launch_pass1(const FFTPlan3& plan, Pass1Mode mode, const Pass1Args& a
 hipError_t launch_pass2(const FFTPlan3& plan, const Pass2Args& a, int batch, hipStream_t s) {
   const uint32_t ntiles = plan.wg2() * static_cast<uint32_t>(batch);
   const dim3 grid(plan.persist_wgs ? std::min(ntiles, plan.persist_wgs) : ntiles);
-  if (!plan.legacy_pass2) {
-    switch (plan.L2) {
+  // register-staged pass 2 where compiled (one LDS crossing per tile), the
+  // generic LDS-staged kernel for the other lengths
+  switch (plan.L2) {
 #define X(n)                                                                                   \
   case n:                                                                                      \
     hipLaunchKernelGGL((pass2r_kernel<n>), grid, dim3(kNcol * (n / 16)), 0, s, a, ntiles);     \
     return hipGetLastError();
-      X(32) X(64) X(128) X(256)
+    X(32) X(64) X(128) X(256)
 #undef X
-      default: break;
-    }
+    default: break;
   }
   switch (plan.L2) {
 #define X(n)                                                                \

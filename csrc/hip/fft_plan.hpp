@@ -20,8 +20,6 @@ struct FFTPlan3 {
   uint32_t L1 = 0, L2 = 0, L3 = 0;
   uint32_t ncol1 = 16, ncol2 = 16, rows3 = 8;  // columns / rows per workgroup
   uint32_t persist_wgs = 0;    // persistent passes: workgroups per launch (0: one per tile)
-  bool legacy_pass1 = false;   // generic LDS-staged pass 1 even when the 3x-padding kernel applies
-  bool legacy_pass2 = false;   // LDS-staged generic pass 2 instead of the register-staged one (A/B testing)
   uint32_t wg1() const { return (L2 * L3) / ncol1; }
   uint32_t wg2() const { return (L1 * L3) / ncol2; }
   // pass 3 (untangle): rows c in [0, C/2] with C = L1*L2

@@ -14,8 +14,6 @@
 // dirty-page flags that the host then scans, each workgroup appends only the
 // (bin, power) pairs above the device threshold to per-level candidate lists
 // (wave-aggregated atomics); the host merges them into the candidate table.
-#include <type_traits>
-
 #include "hip_common.hpp"
 #include "hs_kernels.hpp"
 
@@ -26,8 +24,6 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kHalo = 4;
-constexpr int kSpan = kHsTile + kHalo;
-constexpr int kSpanPad = kSpan + kSpan / 16 + 1;
 __device__ __forceinline__ int sidx(int t) { return t + (t >> 4); }
 
 __device__ __forceinline__ void emit(uint32_t* counter, uint2* list, uint32_t cap, bool pred, uint32_t key,
@@ -46,115 +42,42 @@ __device__ __forceinline__ void emit(uint32_t* counter, uint2* list, uint32_t ca
   }
 }
 
-// LDS staging of the harmonic segments: for harmonic l the tile's bins
-// (l*i + 8) >> 4, i in [i0, i0 + kSpan), form one contiguous run of about
-// l*kSpan/16 bins. All 16 runs (8.5 bins per i in total) are copied into LDS
-// with 16-B loads, so the 16 per-i gathers become LDS reads (conflict free:
-// the lanes of a wave read at most 4l consecutive words). The run of harmonic
-// l starts at the 4-aligned bin lo4(l) and occupies kStageCap(l) floats.
-__host__ __device__ constexpr int stage_cap(int l) { return ((l * (kSpan - 1) / 16 + 5 + 3) / 4) * 4; }
-__host__ __device__ constexpr int stage_off(int l) { return l <= 1 ? 0 : stage_off(l - 1) + stage_cap(l - 1); }
-// per harmonic l: ceil(chunks / threads) load iterations
-__host__ __device__ constexpr int stage_iters(int l) { return (stage_cap(l) / 4 + kThreads - 1) / kThreads; }
-__host__ __device__ constexpr int stage_iters_before(int l) { return l <= 1 ? 0 : stage_iters_before(l - 1) + stage_iters(l - 1); }
-// LDS floats of the kernel staging harmonics 1..smax (S_1..S_4 alias the area)
-__host__ __device__ constexpr int stage_lds_floats(int smax) {
-  return stage_off(smax + 1) > 4 * kSpanPad ? stage_off(smax + 1) : 4 * kSpanPad;
-}
-
-// f(integral_constant<l>, integral_constant<it>, flat iteration base) for
-// l = 1..LMAX and it < stage_iters(l), fully unrolled
-template <int LMAX, int L, int IT, typename F>
-__device__ __forceinline__ void stage_for_each_impl(F&& f) {
-  if constexpr (L <= LMAX) {
-    if constexpr (IT < stage_iters(L)) {
-      f(std::integral_constant<int, L>{}, std::integral_constant<int, IT>{}, stage_iters_before(L));
-      stage_for_each_impl<LMAX, L, IT + 1>(f);
-    } else {
-      stage_for_each_impl<LMAX, L + 1, 0>(f);
-    }
-  }
-}
-template <int LMAX, typename F>
-__device__ __forceinline__ void stage_for_each(F&& f) {
-  stage_for_each_impl<LMAX, 1, 0>(f);
-}
-
 // T = float (exact path) or _Float16 (config 5 spectrum); every element is
-// widened to float before the reference-order float sums. Harmonics 1..SMAX
-// are staged in LDS (their runs are short, l/16 bins per i, and shared by
-// many lanes of a gather), harmonics SMAX+1..16 are gathered per i from
-// global memory: SMAX = 0 gathers all, 16 stages all.
-template <typename T, int SMAX, int TILE>
+// widened to float before the reference-order float sums. Each lane gathers
+// the 16 harmonics of its index straight from global memory: within a wave
+// the lanes of one harmonic read at most 4l+1 consecutive words (1-3 cache
+// lines), and 10 workgroups per CU keep enough gathers in flight.
+// (Measured alternatives -- LDS-staged runs, XCD-contiguous tiles, 4 or 16
+// indices per lane, an MFMA selection-matrix sum -- are kept out of the
+// product in tools/experiments/hs_variants.hip; profiles/hs_variants_r2.txt.)
+template <typename T>
 __global__ void __launch_bounds__(kThreads) harmonic_sum_kernel(HSArgs a) {
 #pragma clang fp contract(off)
-  constexpr bool STAGED = SMAX > 0;
-  static_assert(!STAGED || TILE == kHsTile, "LDS staging is laid out for the default tile");
+  constexpr int TILE = kHsTile;
   static_assert(TILE % 16 == 0, "tiles start at i == 8 mod 16");
   constexpr int SPAN = TILE + kHalo;
   constexpr int SPAN_PAD = SPAN + SPAN / 16 + 1;
-  // staged segments, then (after a barrier) S_1..S_4 over the tile + halo
-  __shared__ __attribute__((aligned(16))) float lds[STAGED ? stage_lds_floats(SMAX) : 4 * SPAN_PAD];
+  __shared__ __attribute__((aligned(16))) float lds[4 * SPAN_PAD];
   float (*sv)[SPAN_PAD] = reinterpret_cast<float (*)[SPAN_PAD]>(lds);
   const int b = blockIdx.y;
   const T* P = reinterpret_cast<const T*>(sizeof(T) == 4 ? static_cast<const void*>(a.ps)
                                                         : static_cast<const void*>(a.ps16)) +
                static_cast<size_t>(b) * a.ps_stride;
-  const uint32_t tile_id = a.xcd != 0 ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
-  const uint32_t i0 = a.i_start + tile_id * TILE;
+  // signed: for windows below 16 the first tile starts before bin 0
+  const int i0 = a.i_start + static_cast<int>(blockIdx.x) * TILE;
+  const int w2 = static_cast<int>(a.w2), fhi = static_cast<int>(a.fhi), hhi = static_cast<int>(a.hhi);
   const float ninf = -__builtin_inff();
-  auto lo4 = [&](uint32_t l) { return ((l * i0 + 8u) >> 4) & ~3u; };
-
-  if constexpr (STAGED) {
-    // harmonic by harmonic (compile-time l: the run's origin is a scalar and
-    // no per-lane selection is needed); every load is issued before the first
-    // LDS write. Chunks past the spectrum's stride read as zero (only i >= hhi
-    // would use them).
-    constexpr int kIters = stage_iters_before(SMAX + 1);
-    float4 v[kIters];
-    stage_for_each<SMAX>([&](auto l_tag, auto it_tag, int it_base) {
-      constexpr int l = decltype(l_tag)::value;
-      constexpr int it = decltype(it_tag)::value;
-      constexpr int nch = stage_cap(l) / 4;
-      const int ch = static_cast<int>(threadIdx.x) + it * kThreads;
-      v[it_base + it] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (ch < nch) {
-        const uint32_t bin = lo4(l) + 4u * static_cast<uint32_t>(ch);
-        if (bin + 4 <= a.ps_stride) {
-          if constexpr (sizeof(T) == 4) {
-            v[it_base + it] = *reinterpret_cast<const float4*>(P + bin);
-          } else {
-            const uint2 h = *reinterpret_cast<const uint2*>(P + bin);
-            const _Float16* hh = reinterpret_cast<const _Float16*>(&h);
-            v[it_base + it] = make_float4(static_cast<float>(hh[0]), static_cast<float>(hh[1]),
-                                          static_cast<float>(hh[2]), static_cast<float>(hh[3]));
-          }
-        }
-      }
-    });
-    stage_for_each<SMAX>([&](auto l_tag, auto it_tag, int it_base) {
-      constexpr int l = decltype(l_tag)::value;
-      constexpr int it = decltype(it_tag)::value;
-      const int ch = static_cast<int>(threadIdx.x) + it * kThreads;
-      if (ch < stage_cap(l) / 4) reinterpret_cast<float4*>(lds + stage_off(l))[ch] = v[it_base + it];
-    });
-    __syncthreads();
-  }
-  auto ld = [&](uint32_t l, uint32_t i) -> float {
-    const uint32_t bin = (l * i + 8u) >> 4;
-    if (static_cast<int>(l) <= SMAX) return lds[stage_off(static_cast<int>(l)) + static_cast<int>(bin - lo4(l))];
-    return static_cast<float>(P[bin]);
-  };
+  auto ld = [&](uint32_t l, uint32_t i) -> float { return static_cast<float>(P[(l * i + 8u) >> 4]); };
 
   constexpr int kIt = (SPAN + kThreads - 1) / kThreads;
   float s1[kIt], s2[kIt], s3[kIt], s4[kIt], p0[kIt];
 #pragma unroll
   for (int it = 0; it < kIt; ++it) {
     const int t = threadIdx.x + it * kThreads;
-    const uint32_t i = i0 + t;
+    const int i = i0 + t;
     s1[it] = s2[it] = s3[it] = s4[it] = ninf;
     p0[it] = 0.0f;
-    if (t < SPAN && i >= a.w2 && i < a.hhi) {
+    if (t < SPAN && i >= w2 && i < hhi) {
       float sum = ld(16, i);
       p0[it] = sum;
       sum += ld(8, i);
@@ -167,7 +90,6 @@ __global__ void __launch_bounds__(kThreads) harmonic_sum_kernel(HSArgs a) {
       s4[it] = sum;
     }
   }
-  if constexpr (STAGED) __syncthreads();  // staging area becomes sv
 #pragma unroll
   for (int it = 0; it < kIt; ++it) {
     const int t = threadIdx.x + it * kThreads;
@@ -188,10 +110,10 @@ __global__ void __launch_bounds__(kThreads) harmonic_sum_kernel(HSArgs a) {
   for (int it = 0; it < kIt; ++it) {
     const int t = threadIdx.x + it * kThreads;
     if (t - static_cast<int>(threadIdx.x) >= TILE) break;  // uniform: whole iterations past the tile
-    const uint32_t i = i0 + t;
-    const bool in = t < TILE && (i >= a.w2 && i < a.fhi);
+    const int i = i0 + t;
+    const bool in = t < TILE && (i >= w2 && i < fhi);
     const float p = in ? p0[it] : 0.0f;
-    emit(count, list, a.cap, in && p > thr0, hs_pack(b, 0, i), p);
+    emit(count, list, a.cap, in && p > thr0, hs_pack(b, 0, static_cast<uint32_t>(i)), p);
   }
   // levels 1..4: group of 2^h consecutive i starting at s == 2^(h-1) mod 2^h;
   // one thread per group, stride-2^h reads made (nearly) conflict free by the
@@ -205,415 +127,37 @@ __global__ void __launch_bounds__(kThreads) harmonic_sum_kernel(HSArgs a) {
     const int ngroups = (TILE - first + g - 1) / g;
     for (int q = threadIdx.x; q < ((ngroups + kThreads - 1) / kThreads) * kThreads; q += kThreads) {
       bool pred = false;
-      uint32_t j = 0;
+      int j = 0;
       float m = ninf;
       if (q < ngroups) {
         const int t0 = first + q * g;
-        j = (i0 + static_cast<uint32_t>(t0) + off) >> h;
-        if (j >= a.w2 && j < a.fhi) {
+        j = (i0 + t0 + off) >> h;  // arithmetic shift: negative groups stay below w2
+        if (j >= w2 && j < fhi) {
 #pragma unroll
           for (int u = 0; u < 16; ++u)
             if (u < g) m = fmaxf(m, sv[h - 1][sidx(t0 + u)]);
           pred = m > thr;
         }
       }
-      emit(count, list, a.cap, pred, hs_pack(b, h, j), m);
+      emit(count, list, a.cap, pred, hs_pack(b, h, static_cast<uint32_t>(j)), m);
     }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Quad harmonic sum: like harmonic_sum_kernel (1008-index tiles, 4-index halo,
-// level maxima from LDS) but each lane sums 4 consecutive indices i_b + r. For
-// harmonic l their bins (l*(i_b + r) + 8) >> 4 lie within 4 words of
-// B = (l*i_b + 8) >> 4, so ONE 16-byte load per harmonic replaces four
-// gathers; the word for r is q or q+1 with q = l*r >> 4, chosen by
-// comparing the lane's phase (l*i_b + 8) & 15 with a constant. A wave's
-// 16-byte loads of harmonic l span 64 l + 16 bytes (l/2 + 2 lines), as
-// compact as the per-i gathers, with a quarter of the instructions.
-__global__ void __launch_bounds__(kThreads) harmonic_sum_q4_kernel(HSArgs a) {
-#pragma clang fp contract(off)
-  constexpr int TILE = 1008;
-  constexpr int SPAN = TILE + kHalo;  // 1012 = 253 lanes x 4
-  constexpr int SPAN_PAD = SPAN + SPAN / 16 + 1;
-  __shared__ __attribute__((aligned(16))) float lds[4 * SPAN_PAD];
-  float (*sv)[SPAN_PAD] = reinterpret_cast<float (*)[SPAN_PAD]>(lds);
-  const int b = blockIdx.y;
-  const uint32_t i0 = a.i_start + blockIdx.x * TILE;
-  const float ninf = -__builtin_inff();
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(a.ps + static_cast<size_t>(b) * a.ps_stride), 0, static_cast<int>(a.ps_stride * 4u), 0x00020000);
-  const int t = threadIdx.x;
-  const uint32_t ib = i0 + 4u * static_cast<uint32_t>(t);
-  float s1[4], s2[4], s3[4], s4[4], p0[4];
-  {
-    // value of harmonic L for index ib + r, r = 0..3
-    auto harm = [&](auto l_tag, float (&v)[4]) {
-      constexpr uint32_t L = decltype(l_tag)::value;
-      const uint32_t x = L * ib + 8u;
-      const uint32_t ph = x & 15u;
-      // words the 4 indices can reach: q + 1 <= (15 + 3L) >> 4
-      constexpr int W = ((15 + 3 * static_cast<int>(L)) >> 4) + 1;
-      float e[4] = {0.f, 0.f, 0.f, 0.f};
-      if constexpr (W == 4) {
-        const auto w = __builtin_amdgcn_raw_buffer_load_b128(rs, 4u * (x >> 4), 0, 0);
-        e[0] = __uint_as_float(w[0]), e[1] = __uint_as_float(w[1]), e[2] = __uint_as_float(w[2]), e[3] = __uint_as_float(w[3]);
-      } else if constexpr (W == 3) {
-        const auto w = __builtin_amdgcn_raw_buffer_load_b96(rs, 4u * (x >> 4), 0, 0);
-        e[0] = __uint_as_float(w[0]), e[1] = __uint_as_float(w[1]), e[2] = __uint_as_float(w[2]);
-      } else {
-        const auto w = __builtin_amdgcn_raw_buffer_load_b64(rs, 4u * (x >> 4), 0, 0);
-        e[0] = __uint_as_float(w[0]), e[1] = __uint_as_float(w[1]);
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const uint32_t lr = L * static_cast<uint32_t>(r);
-        const int q = static_cast<int>(lr >> 4);
-        const uint32_t need = 16u - (lr & 15u);  // phase at which r's bin moves to q + 1
-        v[r] = (q + 1 < W && (lr & 15u) != 0 && ph >= need) ? e[q + 1] : e[q];
-      }
-    };
-    using std::integral_constant;
-    float h16[4], h8[4], h12[4], h4[4], h14[4], h10[4], h6[4], h2[4];
-    float h15[4], h13[4], h11[4], h9[4], h7[4], h5[4], h3[4], h1[4];
-    harm(integral_constant<uint32_t, 16>{}, h16);
-    harm(integral_constant<uint32_t, 8>{}, h8);
-    harm(integral_constant<uint32_t, 12>{}, h12);
-    harm(integral_constant<uint32_t, 4>{}, h4);
-    harm(integral_constant<uint32_t, 14>{}, h14);
-    harm(integral_constant<uint32_t, 10>{}, h10);
-    harm(integral_constant<uint32_t, 6>{}, h6);
-    harm(integral_constant<uint32_t, 2>{}, h2);
-    harm(integral_constant<uint32_t, 15>{}, h15);
-    harm(integral_constant<uint32_t, 13>{}, h13);
-    harm(integral_constant<uint32_t, 11>{}, h11);
-    harm(integral_constant<uint32_t, 9>{}, h9);
-    harm(integral_constant<uint32_t, 7>{}, h7);
-    harm(integral_constant<uint32_t, 5>{}, h5);
-    harm(integral_constant<uint32_t, 3>{}, h3);
-    harm(integral_constant<uint32_t, 1>{}, h1);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const uint32_t i = ib + r;
-      s1[r] = s2[r] = s3[r] = s4[r] = ninf;
-      p0[r] = 0.0f;
-      if (t * 4 + r < SPAN && i >= a.w2 && i < a.hhi) {
-        float sum = h16[r];
-        p0[r] = sum;
-        sum += h8[r];
-        s1[r] = sum;
-        sum += h12[r] + h4[r];
-        s2[r] = sum;
-        sum += h14[r] + h10[r] + h6[r] + h2[r];
-        s3[r] = sum;
-        sum += h15[r] + h13[r] + h11[r] + h9[r] + h7[r] + h5[r] + h3[r] + h1[r];
-        s4[r] = sum;
-      }
-    }
-  }
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int u = 4 * t + r;
-    if (u < SPAN) {
-      sv[0][sidx(u)] = s1[r];
-      sv[1][sidx(u)] = s2[r];
-      sv[2][sidx(u)] = s3[r];
-      sv[3][sidx(u)] = s4[r];
-    }
-  }
-  __syncthreads();
-
-  uint32_t* count = &a.list[0].x;
-  uint2* list = a.list + 1;
-  const float thr0 = a.thr[static_cast<size_t>(b) * kHsThrStride + 0];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int u = 4 * t + r;
-    const uint32_t i = ib + r;
-    const bool in = u < TILE && (i >= a.w2 && i < a.fhi);
-    const float p = in ? p0[r] : 0.0f;
-    emit(count, list, a.cap, in && p > thr0, hs_pack(b, 0, i), p);
-  }
-#pragma unroll
-  for (int h = 1; h <= 4; ++h) {
-    const int g = 1 << h;
-    const int off = g >> 1;
-    const float thr = a.thr[static_cast<size_t>(b) * kHsThrStride + h];
-    const int first = static_cast<int>((off - (i0 % g) + g) % g);
-    const int ngroups = (TILE - first + g - 1) / g;
-    for (int q = threadIdx.x; q < ((ngroups + kThreads - 1) / kThreads) * kThreads; q += kThreads) {
-      bool pred = false;
-      uint32_t j = 0;
-      float m = ninf;
-      if (q < ngroups) {
-        const int t0 = first + q * g;
-        j = (i0 + static_cast<uint32_t>(t0) + off) >> h;
-        if (j >= a.w2 && j < a.fhi) {
-#pragma unroll
-          for (int u = 0; u < 16; ++u)
-            if (u < g) m = fmaxf(m, sv[h - 1][sidx(t0 + u)]);
-          pred = m > thr;
-        }
-      }
-      emit(count, list, a.cap, pred, hs_pack(b, h, j), m);
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Register-blocked harmonic sum (measured slower, BRP_HS_KERNEL=rb). One lane owns the 16 consecutive
-// fundamental-level indices i = 16b + 8 + r (r = 0..15) of "block" b. For
-// harmonic l those read the bins l*b + c_l(r) with the compile-time offsets
-//   c_l(r) = ((l*(8 + r) + 8) >> 4) - ((8l + 8) >> 4),
-// i.e. one contiguous run of n_l = c_l(15) + 1 <= l + 1 words (140 words for
-// all 16 harmonics, 8.75 per i instead of 16 gathers) that the lane fetches
-// with a few 16-byte buffer loads (dword-aligned; the descriptor's range check
-// turns the halo's out-of-range reads into zeros). Every sum is then formed in
-// registers in the reference's float order.
-//
-// The block is the 16-harmonic group j = b + 1 ([16j-8, 16j+8)); it also holds
-// whole groups of the lower levels except one straddling group per level at
-// each end. A lane keeps the partial maximum of its last 1/2/4 indices
-// (levels 1/2/3) and hands it to the next lane (one shuffle per level), which
-// owns the straddling group. Lane 0 of each wave only computes the block
-// before the wave's range for that hand-over: a wave covers 63 blocks
-// (1008 indices), 1.6 % of the loads are the halo.
-namespace rb {
-__host__ __device__ constexpr int c0(int l) { return (8 * l + 8) >> 4; }
-__host__ __device__ constexpr int off(int l, int r) { return ((l * (8 + r) + 8) >> 4) - c0(l); }
-__host__ __device__ constexpr int nrun(int l) { return off(l, 15) + 1; }
-constexpr int kBlocksPerWave = kWave - 1;
-constexpr int kWavesPerGroup = 4;
-
-template <int N>
-__device__ __forceinline__ void load_run(__amdgpu_buffer_rsrc_t rs, uint32_t byte_off, float (&out)[N]) {
-#pragma unroll
-  for (int k = 0; k + 4 <= N; k += 4) {
-    const auto x = __builtin_amdgcn_raw_buffer_load_b128(rs, byte_off + 4u * k, 0, 0);
-    out[k] = __uint_as_float(x[0]);
-    out[k + 1] = __uint_as_float(x[1]);
-    out[k + 2] = __uint_as_float(x[2]);
-    out[k + 3] = __uint_as_float(x[3]);
-  }
-  constexpr int k2 = N & ~3;
-  if constexpr (N - k2 >= 2) {
-    const auto x = __builtin_amdgcn_raw_buffer_load_b64(rs, byte_off + 4u * k2, 0, 0);
-    out[k2] = __uint_as_float(x[0]);
-    out[k2 + 1] = __uint_as_float(x[1]);
-  }
-  if constexpr (N & 1) out[N - 1] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, byte_off + 4u * (N - 1), 0, 0));
-}
-}  // namespace rb
-
-template <int OCC>
-__global__ void __launch_bounds__(kWave * rb::kWavesPerGroup, OCC) harmonic_sum_rb_kernel(HSArgs a) {
-#pragma clang fp contract(off)
-  const int lane = threadIdx.x % kWave;
-  const int wave = blockIdx.x * rb::kWavesPerGroup + threadIdx.x / kWave;
-  const int kb = blockIdx.y;
-  const int w2 = static_cast<int>(a.w2), fhi = static_cast<int>(a.fhi), hhi = static_cast<int>(a.hhi);
-  // first block holding i = w2 (floor division: a window below 8 starts at block -1)
-  const int b_lo = (w2 - 8) >= 0 ? (w2 - 8) / 16 : -((8 - w2 + 15) / 16);
-  const int b = b_lo + wave * rb::kBlocksPerWave + lane - 1;
-  const int i0 = 16 * b + 8;
-  const bool live = i0 + 16 > w2 && i0 < hhi;
-  const float ninf = -__builtin_inff();
-
-  const float* base = a.ps + static_cast<size_t>(kb) * a.ps_stride;
-  const __amdgpu_buffer_rsrc_t rs =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, static_cast<int>(a.ps_stride * 4u), 0x00020000);
-
-  float r16[rb::nrun(16)], r8[rb::nrun(8)], r12[rb::nrun(12)], r4[rb::nrun(4)], r14[rb::nrun(14)], r10[rb::nrun(10)],
-      r6[rb::nrun(6)], r2[rb::nrun(2)], r15[rb::nrun(15)], r13[rb::nrun(13)], r11[rb::nrun(11)], r9[rb::nrun(9)],
-      r7[rb::nrun(7)], r5[rb::nrun(5)], r3[rb::nrun(3)], r1[rb::nrun(1)];
-  // byte offset of the run of harmonic l (negative for the halo of block -1:
-  // wraps past the range check and reads zeros)
-  auto at = [&](int l) { return static_cast<uint32_t>(4 * (l * b + rb::c0(l))); };
-  if (live) {
-    rb::load_run(rs, at(16), r16);
-    rb::load_run(rs, at(8), r8);
-    rb::load_run(rs, at(12), r12);
-    rb::load_run(rs, at(4), r4);
-    rb::load_run(rs, at(14), r14);
-    rb::load_run(rs, at(10), r10);
-    rb::load_run(rs, at(6), r6);
-    rb::load_run(rs, at(2), r2);
-    rb::load_run(rs, at(15), r15);
-    rb::load_run(rs, at(13), r13);
-    rb::load_run(rs, at(11), r11);
-    rb::load_run(rs, at(9), r9);
-    rb::load_run(rs, at(7), r7);
-    rb::load_run(rs, at(5), r5);
-    rb::load_run(rs, at(3), r3);
-    rb::load_run(rs, at(1), r1);
-  } else {
-#define BRP_ZERO(R) _Pragma("unroll") for (int k = 0; k < static_cast<int>(sizeof(R) / 4); ++k) R[k] = 0.0f;
-    BRP_ZERO(r16) BRP_ZERO(r8) BRP_ZERO(r12) BRP_ZERO(r4) BRP_ZERO(r14) BRP_ZERO(r10) BRP_ZERO(r6) BRP_ZERO(r2)
-    BRP_ZERO(r15) BRP_ZERO(r13) BRP_ZERO(r11) BRP_ZERO(r9) BRP_ZERO(r7) BRP_ZERO(r5) BRP_ZERO(r3) BRP_ZERO(r1)
-#undef BRP_ZERO
-  }
-
-  uint32_t* count = &a.list[0].x;
-  uint2* list = a.list + 1;
-  const float* thr = a.thr + static_cast<size_t>(kb) * kHsThrStride;
-  const bool emitter = lane != 0;
-  // index i0 + r contributes to the sums
-  auto valid = [&](int r) { return i0 + r >= w2 && i0 + r < hhi; };
-  auto group_ok = [&](int j) { return emitter && j >= w2 && j < fhi; };
-
-  float acc[16];
-  // level 0: the spectrum itself
-  {
-    const float t0 = thr[0];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      acc[r] = r16[rb::off(16, r)];
-      const int i = i0 + r;
-      const bool ok = emitter && i >= w2 && i < fhi;
-      emit(count, list, a.cap, ok && acc[r] > t0, hs_pack(kb, 0, i), acc[r]);
-    }
-  }
-  auto sv = [&](int r) { return valid(r) ? acc[r] : ninf; };
-  // level 1 (pairs [2j-1, 2j]): groups 8b+5.. 8b+11 in the block, 8b+4 shared with the previous lane
-  {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] += r8[rb::off(8, r)];
-    const float t1 = thr[1];
-    const float tail = __shfl_up(sv(15), 1, kWave);
-    const int jh = 8 * b + 4;
-    const float mh = fmaxf(tail, sv(0));
-    emit(count, list, a.cap, group_ok(jh) && mh > t1, hs_pack(kb, 1, jh), mh);
-#pragma unroll
-    for (int k = 0; k < 7; ++k) {
-      const int j = 8 * b + 5 + k;
-      const float m = fmaxf(sv(2 * k + 1), sv(2 * k + 2));
-      emit(count, list, a.cap, group_ok(j) && m > t1, hs_pack(kb, 1, j), m);
-    }
-  }
-  // level 2 (quads [4j-2, 4j+1]): 4b+3 .. 4b+5 in the block, 4b+2 shared
-  {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const float t = r12[rb::off(12, r)] + r4[rb::off(4, r)];
-      acc[r] += t;
-    }
-    const float t2 = thr[2];
-    const float tail = __shfl_up(fmaxf(sv(14), sv(15)), 1, kWave);
-    const int jh = 4 * b + 2;
-    const float mh = fmaxf(tail, fmaxf(sv(0), sv(1)));
-    emit(count, list, a.cap, group_ok(jh) && mh > t2, hs_pack(kb, 2, jh), mh);
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const int j = 4 * b + 3 + k;
-      const int r = 2 + 4 * k;
-      const float m = fmaxf(fmaxf(sv(r), sv(r + 1)), fmaxf(sv(r + 2), sv(r + 3)));
-      emit(count, list, a.cap, group_ok(j) && m > t2, hs_pack(kb, 2, j), m);
-    }
-  }
-  // level 3 (octets [8j-4, 8j+3]): 2b+2 in the block, 2b+1 shared
-  {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      float t = r14[rb::off(14, r)] + r10[rb::off(10, r)];
-      t += r6[rb::off(6, r)];
-      t += r2[rb::off(2, r)];
-      acc[r] += t;
-    }
-    const float t3 = thr[3];
-    float mt = ninf, mhead = ninf, mfull = ninf;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) mhead = fmaxf(mhead, sv(r));
-#pragma unroll
-    for (int r = 4; r < 12; ++r) mfull = fmaxf(mfull, sv(r));
-#pragma unroll
-    for (int r = 12; r < 16; ++r) mt = fmaxf(mt, sv(r));
-    const float tail = __shfl_up(mt, 1, kWave);
-    const int jh = 2 * b + 1;
-    const float mh = fmaxf(tail, mhead);
-    emit(count, list, a.cap, group_ok(jh) && mh > t3, hs_pack(kb, 3, jh), mh);
-    emit(count, list, a.cap, group_ok(jh + 1) && mfull > t3, hs_pack(kb, 3, jh + 1), mfull);
-  }
-  // level 4 (16 harmonics, [16j-8, 16j+7]): j = b + 1 is the block
-  {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      float t = r15[rb::off(15, r)] + r13[rb::off(13, r)];
-      t += r11[rb::off(11, r)];
-      t += r9[rb::off(9, r)];
-      t += r7[rb::off(7, r)];
-      t += r5[rb::off(5, r)];
-      t += r3[rb::off(3, r)];
-      t += r1[rb::off(1, r)];
-      acc[r] += t;
-    }
-    float m = ninf;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) m = fmaxf(m, sv(r));
-    const int j = b + 1;
-    emit(count, list, a.cap, group_ok(j) && m > thr[4], hs_pack(kb, 4, j), m);
   }
 }
 
 }  // namespace
 
-uint32_t hs_rb_num_groups(uint32_t w2, uint32_t hhi) {
-  if (hhi <= w2) return 0;
-  const int b_lo = (static_cast<int>(w2) - 8) >= 0 ? (static_cast<int>(w2) - 8) / 16
-                                                    : -((8 - static_cast<int>(w2) + 15) / 16);
-  const int b_hi = (static_cast<int>(hhi) - 1 - 8) >= 0 ? (static_cast<int>(hhi) - 1 - 8) / 16 : -1;
-  const uint32_t blocks = static_cast<uint32_t>(b_hi - b_lo + 1);
-  const uint32_t waves = (blocks + rb::kBlocksPerWave - 1) / rb::kBlocksPerWave;
-  return (waves + rb::kWavesPerGroup - 1) / rb::kWavesPerGroup;
-}
-
-uint32_t hs_num_tiles(uint32_t i_start, uint32_t hhi, uint32_t tile) {
-  if (hhi <= i_start) return 0;
-  return (hhi - i_start + tile - 1) / tile;
+uint32_t hs_num_tiles(int32_t i_start, uint32_t hhi) {
+  const int64_t span = static_cast<int64_t>(hhi) - i_start;
+  if (span <= 0) return 0;
+  return static_cast<uint32_t>((span + kHsTile - 1) / kHsTile);
 }
 
 hipError_t launch_harmonic_sum(const HSArgs& a, int batch, hipStream_t s) {
-  if (a.variant == HS_QUAD) {
-    if (a.ps16 != nullptr) return hipErrorInvalidValue;
-    const uint32_t tiles = hs_num_tiles(a.i_start, a.hhi, 1008);
-    if (tiles == 0) return hipSuccess;
-    hipLaunchKernelGGL(harmonic_sum_q4_kernel, dim3(tiles, batch), dim3(kThreads), 0, s, a);
-    return hipGetLastError();
-  }
-  if (a.variant == HS_REGISTER_BLOCKED) {
-    if (a.ps16 != nullptr) return hipErrorInvalidValue;
-    const uint32_t groups = hs_rb_num_groups(a.w2, a.hhi);
-    if (groups == 0) return hipSuccess;
-    const dim3 grid(groups, batch), block(kWave * rb::kWavesPerGroup);
-    switch (a.rb_occupancy) {
-      case 4: hipLaunchKernelGGL(harmonic_sum_rb_kernel<4>, grid, block, 0, s, a); break;
-      default: hipLaunchKernelGGL(harmonic_sum_rb_kernel<1>, grid, block, 0, s, a); break;
-    }
-    return hipGetLastError();
-  }
-  const uint32_t tile = a.tile != 0 ? a.tile : kHsTile;
-  if (a.staged_harmonics != 0 && tile != kHsTile) return hipErrorInvalidValue;
-  const uint32_t tiles = hs_num_tiles(a.i_start, a.hhi, tile);
+  const uint32_t tiles = hs_num_tiles(a.i_start, a.hhi);
   if (tiles == 0) return hipSuccess;
   const dim3 grid(tiles, batch);
-#define BRP_HS_LAUNCH(SM, TL)                                                                                   \
-  if (a.ps16 != nullptr) hipLaunchKernelGGL((harmonic_sum_kernel<_Float16, SM, TL>), grid, dim3(kThreads), 0, s, a); \
-  else hipLaunchKernelGGL((harmonic_sum_kernel<float, SM, TL>), grid, dim3(kThreads), 0, s, a);
-  switch (a.staged_harmonics) {
-    case 0:
-      switch (tile) {
-        case kHsTile: BRP_HS_LAUNCH(0, kHsTile) break;
-        case 1008: BRP_HS_LAUNCH(0, 1008) break;
-        case 2032: BRP_HS_LAUNCH(0, 2032) break;
-        case 496: BRP_HS_LAUNCH(0, 496) break;
-        default: return hipErrorInvalidValue;
-      }
-      break;
-    case 4: BRP_HS_LAUNCH(4, kHsTile) break;
-    case 8: BRP_HS_LAUNCH(8, kHsTile) break;
-    case 16: BRP_HS_LAUNCH(16, kHsTile) break;
-    default: return hipErrorInvalidValue;
-  }
-#undef BRP_HS_LAUNCH
+  if (a.ps16 != nullptr) hipLaunchKernelGGL(harmonic_sum_kernel<_Float16>, grid, dim3(kThreads), 0, s, a);
+  else hipLaunchKernelGGL(harmonic_sum_kernel<float>, grid, dim3(kThreads), 0, s, a);
   return hipGetLastError();
 }
 

@@ -1,5 +1,5 @@
 # Iteration loop: GPU kernel tests, then stage timings under each env setting in $EXPS
-# (space-separated, e.g. EXPS="BRP_P2_LEGACY=1 BRP_PERSIST=6"; "-" = defaults)
+# (space-separated, e.g. EXPS="BRP_PERSIST=6 BRP_SHARE_SERIES=0"; "-" = defaults)
 set -o pipefail
 export TMPDIR=/tmp
 cd $GRAFT_REPO_ROOT

@@ -60,12 +60,11 @@ def test_power_spectrum_bench_size(brp, gpu):
         assert err.max() < 1e-3, (k, err.max(), int(np.argmax(err)) + 1)
 
 
-@pytest.mark.parametrize("variant,window", [("rb", 100), ("rb", 10), ("rb", 1001), ("gather", 100), ("quad", 100), ("quad", 1001)])
-def test_harmonic_sum_matches_cpu_bitwise(brp, gpu, tmp_path, monkeypatch, variant, window):
-    """Same power spectrum in -> identical candidate bins and powers out, for the
-    register-blocked kernel (default; windows below 8 and odd ones included)
-    and the per-i gather kernel."""
-    monkeypatch.setenv("BRP_HS_KERNEL", variant)
+@pytest.mark.parametrize("window", [100, 1001, 16, 10, 0])
+def test_harmonic_sum_matches_cpu_bitwise(brp, gpu, tmp_path, window):
+    """Same power spectrum in -> identical candidate bins and powers out (odd and
+    small running-median windows move the first tile's start; below 16 it lies
+    before bin 0)."""
     case = synth.synthetic_case(tmp_path, n=1 << 17, n_templates=2,
                                 inj=synth.Injection(f0=150.0, P_orb=900.0, tau=0.02, psi0=2.0, amplitude=3.0))
     hdr, series, _ = brp.read_work_unit(case["wu"])
@@ -84,11 +83,9 @@ def test_harmonic_sum_matches_cpu_bitwise(brp, gpu, tmp_path, monkeypatch, varia
         np.testing.assert_array_equal(pw_g, pw_c)
 
 
-@pytest.mark.parametrize("variant", ["rb", "quad", "gather"])
-def test_harmonic_sum_bench_size_matches_cpu_bitwise(brp, gpu, monkeypatch, variant):
-    """Benchmark geometry (hhi = 5.27 M bins, two templates of a batch): every
-    harmonic-sum kernel's candidates equal the CPU model's on the same spectrum."""
-    monkeypatch.setenv("BRP_HS_KERNEL", variant)
+def test_harmonic_sum_bench_size_matches_cpu_bitwise(brp, gpu):
+    """Benchmark geometry (hhi = 5.27 M bins, two templates of a batch): the
+    harmonic-sum candidates equal the CPU model's on the same spectrum."""
     hdr, series, _ = brp.read_work_unit(str(WU))
     opt = dict(OPT_BENCH, white=True)
     geom = brp.derive_geometry(hdr, opt)
@@ -151,29 +148,6 @@ def test_whitening_overlapping_zaps_deterministic(brp, gpu, tmp_path):
     np.testing.assert_array_equal(w1, w2)
     rms = float(np.sqrt(np.mean(w_cpu.astype(np.float64) ** 2)))
     assert np.max(np.abs(w1 - w_cpu)) / rms < 1e-4
-
-
-def test_two_pass_fft_matches_cpu(brp, gpu, monkeypatch):
-    """Opt-in two-pass template transform (BRP_FFT2=1: 768-point gather-fused
-    column pass, 8192-point row-pair pass, slab-major transpose) on the bench
-    geometry vs the CPU golden model, and the full search table vs the default
-    three-pass path on the first templates of the bench bank."""
-    monkeypatch.setenv("BRP_FFT2", "1")
-    hdr, series, _ = brp.read_work_unit(str(WU))
-    opt = dict(OPT_BENCH, white=True)
-    geom = brp.derive_geometry(hdr, opt)
-    eng = _engine(brp, geom, series)
-    series = eng.whiten(opt, brp.read_zaplist(str(ZAP)), series)
-    P, tau, psi = brp.read_template_bank(str(BANK))
-    for k in (0, 3):
-        ps_gpu, ns_gpu = eng.power_spectrum(float(P[k]), float(tau[k]), float(psi[k]))
-        ps_cpu, ns_cpu = _cpu_ps(brp, series, geom, float(P[k]), float(tau[k]), float(psi[k]))
-        assert ns_gpu == ns_cpu
-        lim = geom["harmonic_idx_hi"]
-        scale = float(np.median(ps_cpu[geom["window_2"]:lim]))
-        err = np.abs(ps_gpu[1:lim].astype(np.float64) - ps_cpu[1:lim]) / np.maximum(ps_cpu[1:lim], scale)
-        assert np.percentile(err, 99.9) < 2e-5, (k, np.percentile(err, 99.9))
-        assert err.max() < 1e-3, (k, err.max(), int(np.argmax(err)) + 1)
 
 
 @pytest.mark.parametrize("w", [1, 2, 99, 100, 1000, 3072])

@@ -38,19 +38,28 @@ def _entries(table):
     return [e for e in table.entries() if e[5] > 0]
 
 
-def _compare_tables(t_gpu, t_cpu, rtol=2e-4):
-    """Same candidate bins per level; powers within float-FFT tolerance."""
+def _compare_tables(t_gpu, t_cpu, rtol=2e-4, margin=1e-4):
+    """Same candidate bins per level, both ways, for every entry whose power is
+    more than `margin` (relative) above the level's weakest kept power (the
+    100th power of a full level); powers within float-FFT tolerance. Only
+    entries within `margin` of that boundary may differ (near-ties)."""
     eg, ec = t_gpu.entries(), t_cpu.entries()
     for h in range(5):
         g = {e[0]: e for e in eg[h * 100:(h + 1) * 100] if e[5] > 0}
         c = {e[0]: e for e in ec[h * 100:(h + 1) * 100] if e[5] > 0}
-        # entries at the bottom of a full level may differ by near-ties; require
-        # the strongest 90% to agree exactly in bin
-        strong = sorted(c.values(), key=lambda e: -e[1])[:max(1, int(0.9 * len(c)))]
-        for e in strong:
-            assert e[0] in g, (h, e)
-            assert g[e[0]][1] == pytest.approx(e[1], rel=rtol), (h, e, g[e[0]])
-        assert abs(len(g) - len(c)) <= max(1, len(c) // 10)
+        if not c:  # nothing above the chi^2 threshold on this level
+            assert not g, (h, list(g.values())[:3])
+            continue
+        floor = min(e[1] for e in c.values()) * (1.0 + margin)
+        floor_g = min(e[1] for e in g.values()) * (1.0 + margin) if g else 0.0
+        for e in c.values():
+            if e[1] > floor:
+                assert e[0] in g, (h, e)
+                assert g[e[0]][1] == pytest.approx(e[1], rel=rtol), (h, e, g[e[0]])
+        for e in g.values():
+            if e[1] > max(floor, floor_g):
+                assert e[0] in c, (h, e)
+        assert abs(len(g) - len(c)) <= sum(1 for e in c.values() if e[1] <= floor) + 1
 
 
 @pytest.mark.parametrize("n,padding", [(1 << 15, 1.0), (1 << 16, 2.0), (3 << 14, 3.0), (5 << 14, 1.0)])
@@ -219,23 +228,6 @@ def test_fine_grained_parameter_and_result_buffers(brp, gpu, case, tmp_path):
             assert "large BAR 1" in r.stdout + r.stderr
         runs[fg] = (tmp_path / fg / "res.cand").read_bytes()
     assert runs["in"] == runs["0"] and runs["out"] == runs["0"] and runs["both"] == runs["0"]
-
-
-def test_harmonic_sum_variants_same_result(brp, gpu, case, tmp_path):
-    """Every harmonic-sum kernel instantiation (tiles of 496 / 1008 / 1024 /
-    2032 bins, harmonics staged in LDS, XCD-contiguous tiles) writes the same
-    result file as the default."""
-    variants = {"default": {}, "t496": dict(BRP_HS_TILE="496"), "t1024": dict(BRP_HS_TILE="1024"),
-                "t2032": dict(BRP_HS_TILE="2032"), "s4": dict(BRP_HS_STAGE="4"), "s8": dict(BRP_HS_STAGE="8"),
-                "s16": dict(BRP_HS_STAGE="16"), "xcd": dict(BRP_HS_XCD="1")}
-    runs = {}
-    for name, env in variants.items():
-        r = _app_gpu(case, tmp_path / name, **env)
-        assert r.returncode == 0, (name, r.stderr[-3000:])
-        runs[name] = (tmp_path / name / "res.cand").read_bytes()
-    assert len(runs["default"]) > 0
-    for name, got in runs.items():
-        assert got == runs["default"], name
 
 
 _RCCL_SCRIPT = r"""

@@ -2,13 +2,14 @@
 (debian/extra/create_wisdomf_eah_brp.sh): measures the template pipeline of
 the benchmark geometry on this GPU for candidate kernel settings and writes the
 fastest into data/wisdom/mi355x.json, which the HIP engine reads at setup
-(csrc/core/wisdom.cpp; BRP_PERSIST / BRP_FFT2 / BRP_HS_STAGE still override).
+(csrc/core/wisdom.cpp; BRP_PERSIST still overrides).
 
-Stage 1 (kernel variants, sequential pipeline time per template from
-HipEngine.benchmark_stages): pass-2 persistence, two- vs three-pass FFT,
-LDS-staged harmonics. Stage 2 (concurrency, bench.py on a bank prefix with the
-stage-1 winner): templates per batch x pipelines per GPU; recorded in the file
-for the application defaults.
+Stage 1 (sequential pipeline time per template from HipEngine.benchmark_stages):
+pass-2 persistent workgroups per CU. Stage 2 (concurrency, bench.py on a bank
+prefix with the stage-1 winner): templates per batch x pipelines per GPU;
+recorded in the file for the application defaults. (The two-pass FFT and the
+harmonic-sum variants were measured slower and are not product options:
+profiles/README.md, tools/experiments/.)
 
   python tools/tune_plan.py [--templates 2000] [--out data/wisdom/mi355x.json]
 """
@@ -16,7 +17,6 @@ from __future__ import annotations
 
 import argparse
 import datetime
-import itertools
 import json
 import os
 import subprocess
@@ -71,18 +71,15 @@ def main() -> int:
 
     # stage 1: kernel variants
     results = []
-    for persist, passes, hs in itertools.product((2, 4, 6, 8), (3, 2), (0, 8)):
-        if passes == 2 and persist != 4:
-            continue  # pass 2 (the persistent kernel) does not exist in the two-pass plan
-        env = {"BRP_PERSIST": persist, "BRP_FFT2": 1 if passes == 2 else 0, "BRP_HS_STAGE": hs}
+    for persist in (0, 2, 3, 4, 6, 8):
+        env = {"BRP_PERSIST": persist}
         us = stage_time(brp, geom, series, zaps, tin, env)
-        results.append(dict(persist_per_cu=persist, fft_passes=passes, hs_stage=hs, us_per_template=round(us, 2)))
+        results.append(dict(persist_per_cu=persist, us_per_template=round(us, 2)))
         print(json.dumps(results[-1]), flush=True)
     best = min(results, key=lambda r: r["us_per_template"])
 
     # stage 2: batch x pipelines with the stage-1 winner (subprocess bench runs)
-    env = dict(os.environ, BRP_PERSIST=str(best["persist_per_cu"]), BRP_FFT2="1" if best["fft_passes"] == 2 else "0",
-               BRP_HS_STAGE=str(best["hs_stage"]))
+    env = dict(os.environ, BRP_PERSIST=str(best["persist_per_cu"]))
     conc = []
     for batch, pipes in ((1, 2), (1, 3), (1, 4), (2, 2), (2, 3)):
         r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--steps", "2", "--warmup", "1", "--templates",
@@ -97,24 +94,10 @@ def main() -> int:
         print(json.dumps(conc[-1]), flush=True)
     bc = max(conc, key=lambda r: r["templates_per_s"])
 
-    # stage 3: harmonic-sum tile at the chosen concurrency (no effect in isolation)
-    tiles = []
-    for tile in (1008, 1024, 496):
-        r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--steps", "2", "--warmup", "1", "--templates",
-                            str(args.templates), "--batch", str(bc["batch"]), "--streams", str(bc["pipelines"])],
-                           env=dict(env, BRP_HS_TILE=str(tile)), capture_output=True, text=True, timeout=600)
-        line = [l for l in r.stdout.splitlines() if l.startswith("{")]
-        if r.returncode != 0 or not line:
-            print(r.stderr[-2000:], file=sys.stderr)
-            return 1
-        tiles.append(dict(hs_tile=tile, templates_per_s=json.loads(line[-1])["value"]))
-        print(json.dumps(tiles[-1]), flush=True)
-    bt = max(tiles, key=lambda r: r["templates_per_s"])
-
-    entry = dict(arch=arch, M=int(M), persist_per_cu=best["persist_per_cu"], fft_passes=best["fft_passes"],
-                 hs_stage=best["hs_stage"], hs_tile=bt["hs_tile"], batch=bc["batch"], pipelines=bc["pipelines"],
-                 us_per_template_sequential=best["us_per_template"], templates_per_s=bc["templates_per_s"],
-                 date=datetime.date.today().isoformat(), stage1=results, stage2=conc, stage3=tiles)
+    entry = dict(arch=arch, M=int(M), persist_per_cu=best["persist_per_cu"], batch=bc["batch"],
+                 pipelines=bc["pipelines"], us_per_template_sequential=best["us_per_template"],
+                 templates_per_s=bc["templates_per_s"], date=datetime.date.today().isoformat(), stage1=results,
+                 stage2=conc)
     out = Path(args.out)
     doc = {"entries": []}
     if out.exists():
