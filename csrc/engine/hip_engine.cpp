@@ -392,6 +392,7 @@ struct HipEngine::Impl {
       }
       case kHarmonic: {
         hipk::HSArgs ah{};
+        ah.mode = ps_fp16 ? hipk::HS_F16 : hipk::HS_F32;
         ah.ps = ps.p;
         ah.ps16 = ps_fp16 ? reinterpret_cast<const _Float16*>(ps.p) : nullptr;
         ah.ps_stride = ps_stride;

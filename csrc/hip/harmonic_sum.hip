@@ -42,32 +42,54 @@ __device__ __forceinline__ void emit(uint32_t* counter, uint2* list, uint32_t ca
   }
 }
 
-// T = float (exact path) or _Float16 (config 5 spectrum); every element is
-// widened to float before the reference-order float sums. Each lane gathers
-// the 16 harmonics of its index straight from global memory: within a wave
-// the lanes of one harmonic read at most 4l+1 consecutive words (1-3 cache
-// lines), and 10 workgroups per CU keep enough gathers in flight.
+// MODE HS_F32: fp32 spectrum (exact path). HS_F16: fp16 spectrum (config 5),
+// widened to float before the reference-order float sums.
+//
+// Each lane gathers the 16 harmonics of its index straight from global memory:
+// within a wave the lanes of one harmonic read at most 4l+1 consecutive words
+// (1-3 cache lines), and 10 workgroups per CU keep enough gathers in flight.
 // (Measured alternatives -- LDS-staged runs, XCD-contiguous tiles, 4 or 16
 // indices per lane, an MFMA selection-matrix sum -- are kept out of the
 // product in tools/experiments/hs_variants.hip; profiles/hs_variants_r2.txt.)
-template <typename T>
+template <int MODE>
 __global__ void __launch_bounds__(kThreads) harmonic_sum_kernel(HSArgs a) {
 #pragma clang fp contract(off)
   constexpr int TILE = kHsTile;
   static_assert(TILE % 16 == 0, "tiles start at i == 8 mod 16");
   constexpr int SPAN = TILE + kHalo;
   constexpr int SPAN_PAD = SPAN + SPAN / 16 + 1;
+  constexpr bool kHalf = MODE != HS_F32;
   __shared__ __attribute__((aligned(16))) float lds[4 * SPAN_PAD];
   float (*sv)[SPAN_PAD] = reinterpret_cast<float (*)[SPAN_PAD]>(lds);
   const int b = blockIdx.y;
-  const T* P = reinterpret_cast<const T*>(sizeof(T) == 4 ? static_cast<const void*>(a.ps)
-                                                        : static_cast<const void*>(a.ps16)) +
-               static_cast<size_t>(b) * a.ps_stride;
+  const float* P32 = a.ps + static_cast<size_t>(b) * a.ps_stride;
+  const _Float16* P16 = a.ps16 + static_cast<size_t>(b) * a.ps_stride;
   // signed: for windows below 16 the first tile starts before bin 0
   const int i0 = a.i_start + static_cast<int>(blockIdx.x) * TILE;
   const int w2 = static_cast<int>(a.w2), fhi = static_cast<int>(a.fhi), hhi = static_cast<int>(a.hhi);
   const float ninf = -__builtin_inff();
-  auto ld = [&](uint32_t l, uint32_t i) -> float { return static_cast<float>(P[(l * i + 8u) >> 4]); };
+  // Gathers through a buffer descriptor: per harmonic l the thread computes
+  // its bin offset once, (l (i0 + t) + 8) >> 4; iteration it (index + 256 it)
+  // adds exactly 16 l it bins, an immediate of the load instruction. The
+  // descriptor's range check turns the first tile's negative indices (windows
+  // below 16) into zero reads.
+  constexpr uint32_t kEsz = kHalf ? 2u : 4u;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      kHalf ? static_cast<void*>(const_cast<_Float16*>(P16)) : static_cast<void*>(const_cast<float*>(P32)), 0,
+      static_cast<int>(a.ps_stride * kEsz), 0x00020000);
+  const int ib = i0 + static_cast<int>(threadIdx.x);
+  uint32_t off[17];
+#pragma unroll
+  for (int l = 1; l <= 16; ++l) off[l] = kEsz * static_cast<uint32_t>((l * ib + 8) >> 4);
+  auto ld = [&](int l, int it) -> float {
+    const uint32_t o = off[l] + kEsz * 16u * static_cast<uint32_t>(l * it);
+    if constexpr (kHalf) {
+      const unsigned short bits = __builtin_amdgcn_raw_buffer_load_b16(rs, o, 0, 0);
+      return static_cast<float>(__builtin_bit_cast(_Float16, bits));
+    } else {
+      return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, o, 0, 0));
+    }
+  };
 
   constexpr int kIt = (SPAN + kThreads - 1) / kThreads;
   float s1[kIt], s2[kIt], s3[kIt], s4[kIt], p0[kIt];
@@ -78,15 +100,15 @@ __global__ void __launch_bounds__(kThreads) harmonic_sum_kernel(HSArgs a) {
     s1[it] = s2[it] = s3[it] = s4[it] = ninf;
     p0[it] = 0.0f;
     if (t < SPAN && i >= w2 && i < hhi) {
-      float sum = ld(16, i);
+      float sum = ld(16, it);
       p0[it] = sum;
-      sum += ld(8, i);
+      sum += ld(8, it);
       s1[it] = sum;
-      sum += ld(12, i) + ld(4, i);
+      sum += ld(12, it) + ld(4, it);
       s2[it] = sum;
-      sum += ld(14, i) + ld(10, i) + ld(6, i) + ld(2, i);
+      sum += ld(14, it) + ld(10, it) + ld(6, it) + ld(2, it);
       s3[it] = sum;
-      sum += ld(15, i) + ld(13, i) + ld(11, i) + ld(9, i) + ld(7, i) + ld(5, i) + ld(3, i) + ld(1, i);
+      sum += ld(15, it) + ld(13, it) + ld(11, it) + ld(9, it) + ld(7, it) + ld(5, it) + ld(3, it) + ld(1, it);
       s4[it] = sum;
     }
   }
@@ -156,8 +178,10 @@ hipError_t launch_harmonic_sum(const HSArgs& a, int batch, hipStream_t s) {
   const uint32_t tiles = hs_num_tiles(a.i_start, a.hhi);
   if (tiles == 0) return hipSuccess;
   const dim3 grid(tiles, batch);
-  if (a.ps16 != nullptr) hipLaunchKernelGGL(harmonic_sum_kernel<_Float16>, grid, dim3(kThreads), 0, s, a);
-  else hipLaunchKernelGGL(harmonic_sum_kernel<float>, grid, dim3(kThreads), 0, s, a);
+  switch (a.mode) {
+    case HS_F16: hipLaunchKernelGGL(harmonic_sum_kernel<HS_F16>, grid, dim3(kThreads), 0, s, a); break;
+    default: hipLaunchKernelGGL(harmonic_sum_kernel<HS_F32>, grid, dim3(kThreads), 0, s, a); break;
+  }
   return hipGetLastError();
 }
 

@@ -12,9 +12,15 @@ namespace hipk {
 // 4 x 256 lanes exactly (1024 would leave a fifth pass of 4 lanes; +1.4 %).
 constexpr int kHsTile = 1008;
 
+enum HSMode : int {
+  HS_F32 = 0,  // gathers from the fp32 spectrum (exact)
+  HS_F16 = 1,  // gathers from the fp16 spectrum (config 5)
+};
+
 struct HSArgs {
-  const float* ps;        // [batch][ps_stride]
-  const _Float16* ps16;   // fp16 spectrum (config 5) instead of `ps` when non-null
+  int mode;               // HSMode
+  const float* ps;        // [batch][ps_stride] fp32 spectrum (HS_F32)
+  const _Float16* ps16;   // [batch][ps_stride] fp16 spectrum (HS_F16)
   uint32_t ps_stride;
   uint32_t w2, fhi, hhi;  // window_2, fundamental_idx_hi, harmonic_idx_hi
   int32_t i_start;        // first i of tile 0 (== 8 mod 16, <= w2; -8 for windows below 16)

@@ -55,6 +55,7 @@ struct HSArgs {
   int staged_harmonics;   // harmonics 1..n staged in LDS (0, 4, 8 or 16), the rest gathered per i
   uint32_t tile;          // bins i per workgroup (0 = kHsTile; 496, 1008, 2032 without staging)
   uint32_t xcd;           // nonzero: consecutive tiles on one XCD (shared harmonic lines stay in its L2)
+  int ablate;             // timing ablations of the gather kernel: 1 = no spectrum loads, 2 = no level phase
 };
 
 constexpr uint32_t kHsThrStride = 8;  // floats per template in the threshold array (5 used)
@@ -195,6 +196,7 @@ __global__ void __launch_bounds__(kThreads) harmonic_sum_kernel(HSArgs a) {
   }
   auto ld = [&](uint32_t l, uint32_t i) -> float {
     const uint32_t bin = (l * i + 8u) >> 4;
+    if (a.ablate & 1) return static_cast<float>(bin & 1u) * 1e-3f;  // below every threshold: no emits
     if (static_cast<int>(l) <= SMAX) return lds[stage_off(static_cast<int>(l)) + static_cast<int>(bin - lo4(l))];
     return static_cast<float>(P[bin]);
   };
@@ -246,6 +248,7 @@ __global__ void __launch_bounds__(kThreads) harmonic_sum_kernel(HSArgs a) {
     const float p = in ? p0[it] : 0.0f;
     emit(count, list, a.cap, in && p > thr0, hs_pack(b, 0, i), p);
   }
+  if (a.ablate & 2) return;  // uniform per launch
   // levels 1..4: group of 2^h consecutive i starting at s == 2^(h-1) mod 2^h;
   // one thread per group, stride-2^h reads made (nearly) conflict free by the
   // t + t/16 padding of sv
@@ -828,9 +831,9 @@ int main(int argc, char** argv) {
   HCHECK(hipEventCreate(&e1));
   struct V {
     const char* name;
-    int variant, staged, xcd;
-  } vars[] = {{"gather", HS_GATHER, 0, 0},   {"gather_staged16", HS_GATHER, 16, 0}, {"gather_xcd", HS_GATHER, 0, 1},
-              {"quad", HS_QUAD, 0, 0},       {"rb", HS_REGISTER_BLOCKED, 0, 0},      {"mfma", 3, 0, 0}};
+    int variant, staged, xcd, ablate;
+  } vars[] = {{"gather", HS_GATHER, 0, 0, 0}, {"gather_noloads", HS_GATHER, 0, 0, 1}, {"gather_nolevels", HS_GATHER, 0, 0, 2},   {"gather_staged16", HS_GATHER, 16, 0, 0}, {"gather_xcd", HS_GATHER, 0, 1, 0},
+              {"quad", HS_QUAD, 0, 0, 0},       {"rb", HS_REGISTER_BLOCKED, 0, 0, 0},      {"mfma", 3, 0, 0, 0}};
   std::vector<Cand> ref;
   for (const V& v : vars) {
     HSArgs a{};
@@ -847,6 +850,7 @@ int main(int argc, char** argv) {
     a.staged_harmonics = v.staged;
     a.tile = v.staged ? kHsTile : 1008;
     a.xcd = v.xcd;
+    a.ablate = v.ablate;
     HCHECK(hipMemsetAsync(d_list, 0, sizeof(uint2), st));
     HCHECK(launch_harmonic_sum(a, 1, st));
     HCHECK(hipStreamSynchronize(st));
@@ -866,6 +870,7 @@ int main(int argc, char** argv) {
     float ms = 0;
     HCHECK(hipEventElapsedTime(&ms, e0, e1));
     if (ref.empty()) ref = got;
+    if (v.ablate) got = ref;  // ablations are timing-only (ref: the first, unablated variant)
     // agreement with the gather kernel: identical (key, power), or recall of keys + max rel power diff
     size_t same = 0, common = 0;
     double maxrel = 0;
