@@ -238,6 +238,7 @@ struct HipEngine::Impl {
     graphs.clear();
   }
   DevBuf<float2> buf;           // [batch][M]
+  DevBuf<uint8_t> w_rmed;       // wide-window running-median scratch (whitening)
   DevBuf<float> ps;             // [batch][ps_stride]
   DevBuf<double> partials;      // [batch][wg1]
   DevBuf<double> delta;         // [batch] mean-padding correction
@@ -462,23 +463,28 @@ void hip_set_blocking_sync(bool on) { g_blocking_sync = on; }
 
 int hip_running_median(int device, const std::vector<float>& in, uint32_t W, std::vector<float>& out, int reps,
                        double* ms_per_call) {
-  if (W == 0 || in.size() < W || !hipk::running_median_supported(W)) return RADPUL_EVAL;
+  if (W == 0 || in.size() < W) return RADPUL_EVAL;
   BRP_HIP_CHECK(hipSetDevice(device < 0 ? 0 : device), RADPUL_HIP_DEVICE_SET);
   DevBuf<float> din, dout;
+  DevBuf<uint8_t> scratch;
   int rc;
   const size_t n_out = in.size() - W + 1;
   if ((rc = din.alloc(in.size())) || (rc = dout.alloc(n_out))) return rc;
+  const bool wide = !hipk::running_median_supported(W);
+  const uint32_t n_in = static_cast<uint32_t>(in.size());
+  if (wide && (rc = scratch.alloc(hipk::running_median_wide_scratch_bytes(n_in)))) return rc;
+  auto launch = [&]() {
+    return wide ? hipk::launch_running_median_wide(din.p, n_in, W, dout.p, scratch.p, nullptr)
+                : hipk::launch_running_median(din.p, n_in, W, dout.p, nullptr);
+  };
   BRP_HIP_CHECK(hipMemcpy(din.p, in.data(), in.size() * sizeof(float), hipMemcpyHostToDevice),
                 RADPUL_HIP_MEM_COPY_HOST_DEVICE);
   hipEvent_t e0, e1;
   BRP_HIP_CHECK(hipEventCreate(&e0), RADPUL_HIP_DEVICE_SET);
   BRP_HIP_CHECK(hipEventCreate(&e1), RADPUL_HIP_DEVICE_SET);
-  BRP_HIP_CHECK(hipk::launch_running_median(din.p, static_cast<uint32_t>(in.size()), W, dout.p, nullptr),
-                RADPUL_HIP_KERNEL_INVOKE);
+  BRP_HIP_CHECK(launch(), RADPUL_HIP_KERNEL_INVOKE);
   BRP_HIP_CHECK(hipEventRecord(e0, nullptr), RADPUL_HIP_KERNEL_INVOKE);
-  for (int r = 0; r < reps; ++r)
-    BRP_HIP_CHECK(hipk::launch_running_median(din.p, static_cast<uint32_t>(in.size()), W, dout.p, nullptr),
-                  RADPUL_HIP_KERNEL_INVOKE);
+  for (int r = 0; r < reps; ++r) BRP_HIP_CHECK(launch(), RADPUL_HIP_KERNEL_INVOKE);
   BRP_HIP_CHECK(hipEventRecord(e1, nullptr), RADPUL_HIP_KERNEL_INVOKE);
   BRP_HIP_CHECK(hipEventSynchronize(e1), RADPUL_HIP_KERNEL_INVOKE);
   float ms = 0;
@@ -802,15 +808,11 @@ int HipEngine::whiten(const SearchOptions& opt, const std::vector<ZapRange>& zap
   if (hipk::running_median_supported(opt.window)) {
     BRP_HIP_CHECK(hipk::launch_running_median(psw.p, fft_size, opt.window, med.p, s), RADPUL_HIP_KERNEL_INVOKE);
   } else {
-    // very wide windows: exact host running median
-    std::vector<float> h_ps(fft_size), h_med(white_size);
-    BRP_HIP_CHECK(hipMemcpyAsync(h_ps.data(), psw.p, fft_size * sizeof(float), hipMemcpyDeviceToHost, s),
-                  RADPUL_HIP_MEM_COPY_DEVICE_HOST);
-    BRP_HIP_CHECK(hipStreamSynchronize(s), RADPUL_HIP_MEM_COPY_DEVICE_HOST);
-    running_median(h_ps.data(), fft_size, opt.window, h_med.data());
-    BRP_HIP_CHECK(hipMemcpyAsync(med.p, h_med.data(), white_size * sizeof(float), hipMemcpyHostToDevice, s),
-                  RADPUL_HIP_MEM_COPY_HOST_DEVICE);
-    BRP_HIP_CHECK(hipStreamSynchronize(s), RADPUL_HIP_MEM_COPY_HOST_DEVICE);
+    // wide windows (up to the reference's 250 000): device radix sort + median walk
+    const size_t bytes = hipk::running_median_wide_scratch_bytes(fft_size);
+    if (d.w_rmed.n < bytes && (rc = d.w_rmed.alloc(bytes))) return rc;
+    BRP_HIP_CHECK(hipk::launch_running_median_wide(psw.p, fft_size, opt.window, med.p, d.w_rmed.p, s),
+                  RADPUL_HIP_KERNEL_INVOKE);
   }
   BRP_HIP_CHECK(hipk::launch_whiten_scale(spec.p, med.p, white_size, g.window_2, s), RADPUL_HIP_KERNEL_INVOKE);
   // RFI zapping: noise drawn on the host in the reference order (GSL-compatible RNG)

@@ -185,11 +185,20 @@ hipError_t launch_whiten_power(const float2* spec, uint32_t n, float* ps, hipStr
   return hipGetLastError();
 }
 
-bool running_median_supported(uint32_t W) { return W >= 1 && W <= 3072; }
+// LDS spans: 4096 entries (32 KB) up to W = 3072, 16384 entries (128 KB, one
+// workgroup per CU) up to W = 12288; wider windows: rmed_wide.hip
+bool running_median_supported(uint32_t W) { return W >= 1 && W <= 12288; }
 
 hipError_t launch_running_median(const float* in, uint32_t n_in, uint32_t W, float* med, hipStream_t s) {
   if (!running_median_supported(W) || n_in < W) return hipErrorInvalidValue;
   const uint32_t n_out = n_in - W + 1;
+  if (W > 3072) {
+    constexpr int kSpanL = 16384, kThreadsL = 1024;
+    const uint32_t perL = kSpanL - W + 1;
+    hipLaunchKernelGGL((running_median_kernel<kSpanL, kThreadsL, true>), dim3((n_out + perL - 1) / perL),
+                       dim3(kThreadsL), 0, s, in, n_in, W, med, n_out, perL);
+    return hipGetLastError();
+  }
   constexpr int kSpan = 4096, kThreads = 256;
   const uint32_t per = kSpan - W + 1;
   static const bool plain = std::getenv("BRP_RMED_PLAIN") != nullptr;  // A/B switch

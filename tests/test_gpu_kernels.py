@@ -103,6 +103,22 @@ def test_harmonic_sum_bench_size_matches_cpu_bitwise(brp, gpu):
             np.testing.assert_array_equal(outs[k][h][1], ref[h][1])
 
 
+def test_whitening_wide_window_matches_cpu(brp, gpu, tmp_path):
+    """-B above the LDS kernel's 3072: whitening stays on the device (wide
+    running median) and matches the CPU whitening."""
+    case = synth.synthetic_case(tmp_path, n=1 << 16, n_templates=1)
+    hdr, series, _ = brp.read_work_unit(case["wu"])
+    opt = dict(f0=200.0, padding=3.0, fA=0.08, window=5001, white=True)
+    geom = brp.derive_geometry(hdr, opt)
+    zaps = brp.read_zaplist(case["zap"])
+    w_cpu = brp.cpu_whiten(series, geom, opt, zaps)
+    eng = _engine(brp, geom, series)
+    w_gpu = eng.whiten(opt, zaps, series)
+    rms = float(np.sqrt(np.mean(w_cpu.astype(np.float64) ** 2)))
+    assert rms > 0
+    assert np.max(np.abs(w_gpu - w_cpu)) / rms < 1e-4
+
+
 def test_whitening_matches_cpu(brp, gpu, tmp_path):
     case = synth.synthetic_case(tmp_path, n=1 << 16, n_templates=1)
     hdr, series, _ = brp.read_work_unit(case["wu"])
@@ -150,12 +166,16 @@ def test_whitening_overlapping_zaps_deterministic(brp, gpu, tmp_path):
     assert np.max(np.abs(w1 - w_cpu)) / rms < 1e-4
 
 
-@pytest.mark.parametrize("w", [1, 2, 99, 100, 1000, 3072])
+@pytest.mark.parametrize("w", [1, 2, 99, 100, 1000, 3072, 3073, 4096, 10001, 12288, 12289, 65536, 250000])
 def test_running_median_kernel_bit_exact(brp, gpu, w):
-    """Device running median == host Mohanty running median, bit for bit, with ties."""
+    """Device running median == host running median, bit for bit, with ties.
+    Windows above 3072 take the wide path (global radix sort + median walk,
+    rmed_wide.hip) up to the reference's limit of 250 000."""
     rng = np.random.default_rng(w)
-    x = rng.exponential(size=50_000 + 3 * w).astype(np.float32)
+    n = 50_000 + 3 * w if w <= 3072 else w + 30_000
+    x = rng.exponential(size=n).astype(np.float32)
     x[::7] = np.round(x[::7], 1)  # many exact ties
+    x[100:400] = 0.25  # a run of equal values
     ref = brp.running_median(x, w)
     got, _ = brp.hip_running_median(x, w)
     assert got.shape == ref.shape
