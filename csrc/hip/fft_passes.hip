@@ -479,6 +479,54 @@ __device__ __forceinline__ RowTw row_twiddles(const TwiddleTable& tw, uint32_t c
   return r;
 }
 
+// Output of one untangled bin: X_k (+ delta * S_k) -> |X_k|^2 / N (fp32 or
+// fp16 spectrum), or the complex bin. S_k = -(sin(pi n_s k/N) / sin(pi k/N))
+// e^{-i pi (n_s-1) k/N} from ta = W_2N^{n_s k}, tk = W_2N^k.
+template <int MODE>
+struct P3Emit {
+  static constexpr bool kPower = (MODE == P3_POWER || MODE == P3_POWER16);
+  const Pass3Args& a;
+  float dS;
+  bool correct;
+  int b;
+  __device__ __forceinline__ float power(uint32_t k, float2 x, float2 tk, float2 ta) const {
+    if (k == 0) return 0.0f;
+    if (correct) {
+      const float ratio = ta.y * __builtin_amdgcn_rcpf(tk.y);  // v_rcp_f32 (1 ulp)
+      const float2 tc = cmul(ta, conjf2(tk));                  // W_2N^{(n_s-1) k}
+      x = make_float2(x.x - dS * ratio * tc.x, x.y - dS * ratio * tc.y);
+    }
+    return (x.x * x.x + x.y * x.y) * a.norm;
+  }
+  __device__ __forceinline__ void store(uint32_t k, float p) const {
+    const size_t o = static_cast<size_t>(b) * a.ps_stride + k;
+    if (MODE == P3_POWER16) a.ps16[o] = static_cast<_Float16>(p);
+    else a.ps[o] = p;
+  }
+  __device__ __forceinline__ void operator()(uint32_t k, float2 x, float2 tk, float2 ta) const {
+    if (k >= a.limit) return;
+    if (kPower) store(k, power(k, x, tk, ta));
+    else a.spec[k] = x;
+  }
+  // Nyquist bin M: X_M = Re Z_0 - Im Z_0
+  __device__ __forceinline__ void nyquist(float2 z0, uint32_t n_s) const {
+    if (a.M >= a.limit) return;
+    float2 x = make_float2(z0.x - z0.y, 0.0f);
+    if (kPower) {
+      if (correct) {
+        const float2 sp = padding_spectrum(a.tw, n_s, a.M);
+        x = make_float2(x.x + dS * sp.x, x.y + dS * sp.y);
+      }
+      const float pm = (x.x * x.x + x.y * x.y) * a.norm;
+      const size_t o = static_cast<size_t>(b) * a.ps_stride + a.M;
+      if (MODE == P3_POWER16) a.ps16[o] = static_cast<_Float16>(pm);
+      else a.ps[o] = pm;
+    } else {
+      a.spec[a.M] = x;
+    }
+  }
+};
+
 template <int L, int ROWS, int MODE>
 __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Args a) {
   constexpr int TPC = tpc_for<L>();
@@ -565,31 +613,9 @@ __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Arg
   if constexpr (kRegStage1) BlockFFT<L, NSLOT, TPC, true>::run_rest(data, twl);
   else BlockFFT<L, NSLOT, TPC, true>::run(data, twl);
 
-  const float dS = static_cast<float>(delta);
   constexpr bool kPower = (MODE == P3_POWER || MODE == P3_POWER16);
   const bool correct = kPower && n_s > 0;
-  float* ps = a.ps + static_cast<size_t>(b) * a.ps_stride;
-  _Float16* ps16 = a.ps16 ? a.ps16 + static_cast<size_t>(b) * a.ps_stride : nullptr;
-  // X_k (+ delta * S_k) -> |X_k|^2 / N, or the complex bin
-  // S_k = -(sin(pi n_s k/N) / sin(pi k/N)) e^{-i pi (n_s-1) k/N} from ta = W_2N^{n_s k}, tk = W_2N^k
-  auto emit = [&](uint32_t k, float2 x, float2 tk, float2 ta) {
-    if (k >= a.limit) return;
-    if (kPower) {
-      float p = 0.0f;
-      if (k != 0) {
-        if (correct) {
-          const float ratio = ta.y * __builtin_amdgcn_rcpf(tk.y);  // v_rcp_f32 (1 ulp)
-          const float2 tc = cmul(ta, conjf2(tk));  // W_2N^{(n_s-1) k}
-          x = make_float2(x.x - dS * ratio * tc.x, x.y - dS * ratio * tc.y);
-        }
-        p = (x.x * x.x + x.y * x.y) * a.norm;
-      }
-      if (MODE == P3_POWER16) ps16[k] = static_cast<_Float16>(p);
-      else ps[k] = p;
-    } else {
-      a.spec[k] = x;
-    }
-  };
+  P3Emit<MODE> emit{a, static_cast<float>(delta), correct, b};
 
   // untangle: thread -> (slot s, k3 stream), rows c <= C/2 own their bins;
   // bin M-k of the mirror row reuses the twiddles of bin k:
@@ -626,21 +652,7 @@ __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Arg
         const float2 tam = rot_mi(conjf2(ta), n_s);
         emit(kk, untangle_w(zm, zk, wm), tkm, tam);
       }
-      if (c == 0 && k3 == 0 && a.M < a.limit) {
-        // Nyquist bin M: X_M = Re Z_0 - Im Z_0
-        float2 x = make_float2(zk.x - zk.y, 0.0f);
-        if (kPower) {
-          if (correct) {
-            const float2 sp = padding_spectrum(a.tw, n_s, a.M);
-            x = make_float2(x.x + dS * sp.x, x.y + dS * sp.y);
-          }
-          const float pm = (x.x * x.x + x.y * x.y) * a.norm;
-          if (MODE == P3_POWER16) ps16[a.M] = static_cast<_Float16>(pm);
-          else ps[a.M] = pm;
-        } else {
-          a.spec[a.M] = x;
-        }
-      }
+      if (c == 0 && k3 == 0) emit.nyquist(zk, n_s);
     }
   }
 }
