@@ -240,6 +240,8 @@ struct HipEngine::Impl {
   DevBuf<float2> buf;           // [batch][M]
   DevBuf<uint8_t> w_rmed;       // wide-window running-median scratch (whitening)
   DevBuf<float> ps;             // [batch][ps_stride]
+  DevBuf<float> pyr;            // [batch][hs_pyr_stride(ps_stride)]: 8-bin maxima of the spectrum (pruned HS)
+  bool hs_prune = true;         // pruned harmonic sum (BRP_HS_FULL=1: every block exactly)
   DevBuf<double> partials;      // [batch][wg1]
   DevBuf<double> delta;         // [batch] mean-padding correction
   // per-batch input, ONE host->device copy: thresholds | templates
@@ -404,6 +406,9 @@ struct HipEngine::Impl {
         ah.thr = thr.p;
         ah.list = cands.p;
         ah.cap = cap;
+        ah.prune = hs_prune && !ps_fp16;
+        ah.pyr = pyr.p;
+        ah.pyr_stride = hipk::hs_pyr_stride(ps_stride);
         return hipk::launch_harmonic_sum(ah, nb, stream);
       }
       case kEpilogue:
@@ -616,6 +621,8 @@ int HipEngine::setup_impl(const SearchGeometry& g, const float* host_series, con
   if ((rc = d.series.alloc(static_cast<size_t>(d.slots) * g.n_unpadded))) return rc;
   if ((rc = d.buf.alloc(B * d.plan.M))) return rc;
   if ((rc = d.ps.alloc(B * d.ps_stride))) return rc;
+  d.hs_prune = std::getenv("BRP_HS_FULL") == nullptr || std::atoi(std::getenv("BRP_HS_FULL")) == 0;
+  if ((rc = d.pyr.alloc(B * hipk::hs_pyr_stride(d.ps_stride)))) return rc;
   if ((rc = d.partials.alloc(B * d.plan.wg1()))) return rc;
   if ((rc = d.delta.alloc(B))) return rc;
   if (B > hipk::kHsMaxBatch || g.fundamental_idx_hi >= (1u << hipk::kHsBinBits)) {

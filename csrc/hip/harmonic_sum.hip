@@ -14,6 +14,8 @@
 // dirty-page flags that the host then scans, each workgroup appends only the
 // (bin, power) pairs above the device threshold to per-level candidate lists
 // (wave-aggregated atomics); the host merges them into the candidate table.
+#include <utility>
+
 #include "hip_common.hpp"
 #include "hs_kernels.hpp"
 
@@ -166,7 +168,238 @@ __global__ void __launch_bounds__(kThreads) harmonic_sum_kernel(HSArgs a) {
   }
 }
 
+// ------------------------------------------------------------ pruned path
+// The emission thresholds sit far above almost every harmonic sum (the
+// chi^2 false-alarm levels of the reference, or the table floor once it is
+// full), so the exact sums are only needed where some sum can reach one.
+// Float addition is monotonic (a <= a', b <= b' => fl(a+b) <= fl(a'+b')), so
+// summing, in the reference order, the maximum of every harmonic over the
+// bins a 16-index block touches gives an upper bound of every level value the
+// block owns; blocks whose bounds all stay at or below their thresholds emit
+// nothing and are skipped. Harmonics 4..16 take their maxima from 8-bin cells
+// (hs_cells_kernel), 1..3 from the spectrum: a wave's 64 blocks read ~1500
+// contiguous words instead of 16 x 1024 gathers. On the benchmark WU about
+// 2 % of the blocks pass (level 4; profiles/hs_prune_r2.txt); those are then
+// computed exactly like harmonic_sum_kernel does, so the candidate lists are
+// the same (tests/test_gpu_kernels.py, bit for bit against the CPU model).
+constexpr int kBlk = 16;      // indices per block: one level-4 group
+constexpr int kBlkSpan = 20;  // + the 4-index reach of the level-1..3 groups whose first index lies in it
+constexpr int kWaveSpan = kWave * kBlk + (kBlkSpan - kBlk);  // indices a wave's 64 blocks reach
+
+__global__ void __launch_bounds__(256) hs_cells_kernel(HSArgs a) {
+  const int b = blockIdx.y;
+  const uint32_t m = blockIdx.x * 256u + threadIdx.x;  // 8-bin cell
+  if (m >= hs_pyr_stride(a.ps_stride)) return;
+  const float* P = a.ps + static_cast<size_t>(b) * a.ps_stride;
+  const uint32_t k0 = 8u * m;
+  float v[8];
+  if (k0 + 8 <= a.hhi) {
+    const float4 x = reinterpret_cast<const float4*>(P + k0)[0];
+    const float4 y = reinterpret_cast<const float4*>(P + k0)[1];
+    v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+    v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = (k0 + e < a.hhi) ? P[k0 + e] : 0.0f;  // never read by the exact sums
+  }
+  a.pyr[static_cast<size_t>(b) * a.pyr_stride + m] =
+      fmaxf(fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])), fmaxf(fmaxf(v[4], v[5]), fmaxf(v[6], v[7])));
+}
+
+// harmonics in the reference summation order, their source (0: spectrum,
+// 3: 8-bin cells) and their slice of a wave's staging buffer
+constexpr int kHarm[16] = {16, 8, 12, 4, 14, 10, 6, 2, 15, 13, 11, 9, 7, 5, 3, 1};
+constexpr int hs_lvl(int l) { return l >= 4 ? 3 : 0; }
+constexpr int hs_wave_cells(int l) { return (((l * (kWaveSpan - 1) + 15) / 16) >> hs_lvl(l)) + 2; }
+constexpr int hs_slice(int q) {
+  int o = 0;
+  for (int r = 0; r < q; ++r) o += hs_wave_cells(kHarm[r]);
+  return o;
+}
+constexpr int kWaveCells = hs_slice(16);
+
+__device__ __forceinline__ uint32_t hs_cell(int l, int k, int32_t i) {
+  return (static_cast<uint32_t>(l * (i < 0 ? 0 : i) + 8) >> 4) >> k;
+}
+
+// the cells harmonic kHarm[Q] of the wave's blocks reach, contiguous: every
+// lane loads its words of all 16 slices first (unconditional, clamped
+// addresses: a guarded load per word made the compiler wait for each one
+// before its LDS write), then writes them to the wave's staging buffer
+constexpr int hs_chunks(int q) { return (hs_wave_cells(kHarm[q]) + kWave - 1) / kWave; }
+constexpr int hs_chunk0(int q) {
+  int o = 0;
+  for (int r = 0; r < q; ++r) o += hs_chunks(r);
+  return o;
+}
+constexpr int kStageLoads = hs_chunk0(16);
+
+template <int Q>
+__device__ __forceinline__ void hs_load(float* v, const float* P, const float* C8, uint32_t n8, uint32_t nps,
+                                        int32_t I0, int lane) {
+  constexpr int L = kHarm[Q], K = hs_lvl(L);
+  const float* src = K ? C8 : P;
+  const uint32_t lim = K ? n8 : nps;
+  const uint32_t c0 = hs_cell(L, K, I0);
+#pragma unroll
+  for (int q = 0; q < hs_chunks(Q); ++q) {
+    const uint32_t c = c0 + static_cast<uint32_t>(lane + kWave * q);
+    const float x = src[min(c, lim - 1)];
+    v[hs_chunk0(Q) + q] = c < lim ? x : 0.0f;
+  }
+}
+
+template <int Q>
+__device__ __forceinline__ void hs_store(float* buf, const float* v, int lane) {
+  constexpr int N = hs_wave_cells(kHarm[Q]);
+#pragma unroll
+  for (int q = 0; q < hs_chunks(Q); ++q) {
+    const int e = lane + kWave * q;
+    if (e < N) buf[hs_slice(Q) + e] = v[hs_chunk0(Q) + q];
+  }
+}
+
+// max of harmonic kHarm[Q] over the block [ib, ib + kBlkSpan) from the staged cells
+template <int Q>
+__device__ __forceinline__ float hs_block_max(const float* buf, int32_t I0, int32_t ib) {
+  constexpr int L = kHarm[Q], K = hs_lvl(L);
+  constexpr int kCells = (((L * (kBlkSpan - 1) + 15) / 16) >> K) + 2;
+  const float* s = buf + hs_slice(Q) - hs_cell(L, K, I0);
+  const uint32_t lo = hs_cell(L, K, ib), hi = hs_cell(L, K, ib + kBlkSpan - 1);
+  float m = s[lo];
+#pragma unroll
+  for (int d = 1; d < kCells; ++d) m = fmaxf(m, s[min(lo + d, hi)]);
+  return m;
+}
+
+template <int... Q>
+__device__ __forceinline__ void hs_stage_all(std::integer_sequence<int, Q...>, float* buf, const float* P,
+                                             const float* C8, uint32_t n8, uint32_t nps, int32_t I0, int lane) {
+  float v[kStageLoads];
+  (hs_load<Q>(v, P, C8, n8, nps, I0, lane), ...);
+  (hs_store<Q>(buf, v, lane), ...);
+}
+
+// One thread per 16-index block computes the bounds; the wave then computes
+// its flagged blocks exactly, three at a time (lanes 20 s .. 20 s + 19 hold
+// indices ib .. ib + 19 of block s), with the sums, level maxima and emission
+// of harmonic_sum_kernel for the groups whose first index lies in the block.
+// (No global block list: an atomic per wave on one counter serialised a first
+// version at 39 us.)
+__global__ void __launch_bounds__(256) hs_pruned_kernel(HSArgs a, uint32_t nblk) {
+#pragma clang fp contract(off)
+  constexpr int kSubs = kWave / kBlkSpan;  // 3
+  __shared__ float stage[4][kWaveCells];
+  __shared__ float sv[4][kSubs][4][kBlkSpan];
+  const int b = blockIdx.y;
+  const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+  const uint32_t wave_blk0 = blockIdx.x * 256u + static_cast<uint32_t>(wave * kWave);
+  if (wave_blk0 >= nblk) return;  // whole wave
+  const uint32_t blk = wave_blk0 + lane;
+  const float* P = a.ps + static_cast<size_t>(b) * a.ps_stride;
+  const float* thr = a.thr + static_cast<size_t>(b) * kHsThrStride;
+  const int w2 = static_cast<int>(a.w2), fhi = static_cast<int>(a.fhi), hhi = static_cast<int>(a.hhi);
+  const int32_t I0 = a.i_start + static_cast<int32_t>(kBlk * wave_blk0);
+  float* buf = stage[wave];
+  hs_stage_all(std::make_integer_sequence<int, 16>{}, buf, P, a.pyr + static_cast<size_t>(b) * a.pyr_stride,
+               a.pyr_stride, a.ps_stride, I0, lane);
+  // LDS operations of one wave complete in order; keep the compiler from moving them
+  auto wave_sync = [] {
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __builtin_amdgcn_wave_barrier();
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  };
+  wave_sync();
+  bool flag = false;
+  if (blk < nblk) {
+    const int32_t ib = I0 + kBlk * lane;
+    // per-level bounds in the reference summation order (see harmonic_sum_kernel)
+    const float u0 = hs_block_max<0>(buf, I0, ib);
+    const float u1 = u0 + hs_block_max<1>(buf, I0, ib);
+    const float u2 = u1 + (hs_block_max<2>(buf, I0, ib) + hs_block_max<3>(buf, I0, ib));
+    const float u3 = u2 + (((hs_block_max<4>(buf, I0, ib) + hs_block_max<5>(buf, I0, ib)) +
+                            hs_block_max<6>(buf, I0, ib)) + hs_block_max<7>(buf, I0, ib));
+    const float u4 =
+        u3 + (((((((hs_block_max<8>(buf, I0, ib) + hs_block_max<9>(buf, I0, ib)) + hs_block_max<10>(buf, I0, ib)) +
+                  hs_block_max<11>(buf, I0, ib)) + hs_block_max<12>(buf, I0, ib)) + hs_block_max<13>(buf, I0, ib)) +
+               hs_block_max<14>(buf, I0, ib)) + hs_block_max<15>(buf, I0, ib));
+    const float u[5] = {u0, u1, u2, u3, u4};
+#pragma unroll
+    for (int h = 0; h <= 4; ++h) {
+      const int off = h ? 1 << (h - 1) : 0;
+      const int j_lo = (ib + off) >> h, j_hi = (ib + kBlk - 1 + off) >> h;  // groups whose first index is in the block
+      flag |= (j_hi >= w2 && j_lo < fhi) && !(u[h] <= thr[h]);             // NaN bounds are kept
+    }
+  }
+  unsigned long long mask = __ballot(flag);
+  if (mask == 0) return;
+
+  const int sub = lane / kBlkSpan, li = lane % kBlkSpan;
+  const float ninf = -__builtin_inff();
+  uint32_t* count = &a.list[0].x;
+  uint2* list = a.list + 1;
+  while (mask != 0) {  // wave-uniform
+    // the next three flagged blocks of the wave go to subs 0, 1, 2
+    int bit = -1;
+#pragma unroll
+    for (int s = 0; s < kSubs; ++s) {
+      const int f = mask ? __ffsll(static_cast<long long>(mask)) - 1 : -1;
+      if (f >= 0) mask &= mask - 1;
+      if (s == sub) bit = f;
+    }
+    const bool act = sub < kSubs && bit >= 0;
+    const int32_t ib = I0 + kBlk * (act ? bit : 0);
+    const int i = ib + li;
+    float s1 = ninf, s2 = ninf, s3 = ninf, s4 = ninf, p0 = 0.0f;
+    if (act && i >= w2 && i < hhi) {
+      auto ld = [&](int l) { return P[(l * i + 8) >> 4]; };
+      float sum = ld(16);
+      p0 = sum;
+      sum += ld(8);
+      s1 = sum;
+      sum += ld(12) + ld(4);
+      s2 = sum;
+      sum += ld(14) + ld(10) + ld(6) + ld(2);
+      s3 = sum;
+      sum += ld(15) + ld(13) + ld(11) + ld(9) + ld(7) + ld(5) + ld(3) + ld(1);
+      s4 = sum;
+    }
+    if (sub < kSubs) {
+      sv[wave][sub][0][li] = s1;
+      sv[wave][sub][1][li] = s2;
+      sv[wave][sub][2][li] = s3;
+      sv[wave][sub][3][li] = s4;
+    }
+    wave_sync();
+    // level 0: the spectrum itself, indices of the block
+    const bool in0 = act && li < kBlk && i >= w2 && i < fhi;
+    emit(count, list, a.cap, in0 && p0 > thr[0], hs_pack(b, 0, static_cast<uint32_t>(i)), p0);
+    // levels 1..4: lane li < 15 owns one group (8 of level 1, 4 of level 2, 2 of level 3, 1 of level 4)
+    int h = 4, t0 = 0;
+    if (li < 8) { h = 1; t0 = 2 * li + 1; }
+    else if (li < 12) { h = 2; t0 = 4 * (li - 8) + 2; }
+    else if (li < 14) { h = 3; t0 = 8 * (li - 12) + 4; }
+    const int g = 1 << h;
+    float m = ninf;
+    bool pred = false;
+    int j = 0;
+    if (act && li < 15) {
+      for (int q = 0; q < g; ++q) m = fmaxf(m, sv[wave][sub][h - 1][t0 + q]);
+      j = (ib + t0 + (g >> 1)) >> h;
+      pred = j >= w2 && j < fhi && m > thr[h];
+    }
+    emit(count, list, a.cap, pred, hs_pack(b, static_cast<uint32_t>(h), static_cast<uint32_t>(j)), m);
+    wave_sync();
+  }
+}
+
 }  // namespace
+
+uint32_t hs_num_blocks(int32_t i_start, uint32_t hhi) {
+  const int64_t span = static_cast<int64_t>(hhi) - i_start;
+  if (span <= 0) return 0;
+  return static_cast<uint32_t>((span + kBlk - 1) / kBlk);
+}
 
 uint32_t hs_num_tiles(int32_t i_start, uint32_t hhi) {
   const int64_t span = static_cast<int64_t>(hhi) - i_start;
@@ -175,6 +408,13 @@ uint32_t hs_num_tiles(int32_t i_start, uint32_t hhi) {
 }
 
 hipError_t launch_harmonic_sum(const HSArgs& a, int batch, hipStream_t s) {
+  if (a.prune && a.mode == HS_F32) {
+    const uint32_t nblk = hs_num_blocks(a.i_start, a.hhi);
+    if (nblk == 0) return hipSuccess;
+    hipLaunchKernelGGL(hs_cells_kernel, dim3((hs_pyr_stride(a.ps_stride) + 255) / 256, batch), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(hs_pruned_kernel, dim3((nblk + 255) / 256, batch), dim3(256), 0, s, a, nblk);
+    return hipGetLastError();
+  }
   const uint32_t tiles = hs_num_tiles(a.i_start, a.hhi);
   if (tiles == 0) return hipSuccess;
   const dim3 grid(tiles, batch);

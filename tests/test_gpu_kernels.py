@@ -60,11 +60,14 @@ def test_power_spectrum_bench_size(brp, gpu):
         assert err.max() < 1e-3, (k, err.max(), int(np.argmax(err)) + 1)
 
 
+@pytest.mark.parametrize("full", ["0", "1"])
 @pytest.mark.parametrize("window", [100, 1001, 16, 10, 0])
-def test_harmonic_sum_matches_cpu_bitwise(brp, gpu, tmp_path, window):
+def test_harmonic_sum_matches_cpu_bitwise(brp, gpu, tmp_path, monkeypatch, window, full):
     """Same power spectrum in -> identical candidate bins and powers out (odd and
     small running-median windows move the first tile's start; below 16 it lies
-    before bin 0)."""
+    before bin 0). Pruned path (bound filter + exact blocks, default) and the
+    full gather kernel (BRP_HS_FULL=1); the low thresholds flag most blocks."""
+    monkeypatch.setenv("BRP_HS_FULL", full)
     case = synth.synthetic_case(tmp_path, n=1 << 17, n_templates=2,
                                 inj=synth.Injection(f0=150.0, P_orb=900.0, tau=0.02, psi0=2.0, amplitude=3.0))
     hdr, series, _ = brp.read_work_unit(case["wu"])
@@ -83,22 +86,28 @@ def test_harmonic_sum_matches_cpu_bitwise(brp, gpu, tmp_path, window):
         np.testing.assert_array_equal(pw_g, pw_c)
 
 
-def test_harmonic_sum_bench_size_matches_cpu_bitwise(brp, gpu):
+@pytest.mark.parametrize("full,thr", [("0", (9.0, 12.0, 16.0, 22.0, 33.0)), ("1", (9.0, 12.0, 16.0, 22.0, 33.0)),
+                                      ("0", (11.0, 12.5, 15.5, 21.0, 31.0)), ("0", (13.0, 15.0, 18.0, 24.0, 34.5))])
+def test_harmonic_sum_bench_size_matches_cpu_bitwise(brp, gpu, monkeypatch, full, thr):
     """Benchmark geometry (hhi = 5.27 M bins, two templates of a batch): the
-    harmonic-sum candidates equal the CPU model's on the same spectrum."""
+    harmonic-sum candidates equal the CPU model's on the same spectrum, for the
+    pruned path at thresholds that flag many / some / few blocks and for the
+    full gather kernel."""
+    monkeypatch.setenv("BRP_HS_FULL", full)
     hdr, series, _ = brp.read_work_unit(str(WU))
     opt = dict(OPT_BENCH, white=True)
     geom = brp.derive_geometry(hdr, opt)
     eng = _engine(brp, geom, series, batch=2)
     series = eng.whiten(opt, brp.read_zaplist(str(ZAP)), series)
     P, tau, psi = brp.read_template_bank(str(BANK))
-    thr = [9.0, 12.0, 16.0, 22.0, 33.0]
+    thr = list(thr)
     outs = eng.process(P[:2].astype(np.float32), tau[:2].astype(np.float32), psi[:2].astype(np.float32), thr)
     for k in range(2):
         ps_gpu, _ = eng.power_spectrum(float(np.float32(P[k])), float(np.float32(tau[k])), float(np.float32(psi[k])))
         ref, _ = brp.cpu_harmonic_sum(ps_gpu, geom, thr)
+        assert sum(len(ref[h][0]) for h in range(5)) > 0
         for h in range(5):
-            assert len(ref[h][0]) > 0
+            assert len(ref[h][0]) > 0 or thr[0] > 10.0
             np.testing.assert_array_equal(outs[k][h][0], ref[h][0])
             np.testing.assert_array_equal(outs[k][h][1], ref[h][1])
 
