@@ -242,6 +242,8 @@ struct HipEngine::Impl {
   DevBuf<float> ps;             // [batch][ps_stride]
   DevBuf<float> pyr;            // [batch][hs_pyr_stride(ps_stride)]: 8-bin maxima of the spectrum (pruned HS)
   bool hs_prune = true;         // pruned harmonic sum (BRP_HS_FULL=1: every block exactly)
+  int hs_cell_shift = 3;        // its bound cells: 8 bins (BRP_HS_CELL=4: 4 bins, tighter bounds but
+                                // 44 KB LDS / 125 VGPRs per workgroup: 16.4-16.7k vs 15.6-15.8k templates/s)
   DevBuf<double> partials;      // [batch][wg1]
   DevBuf<double> delta;         // [batch] mean-padding correction
   // per-batch input, ONE host->device copy: thresholds | templates
@@ -407,6 +409,7 @@ struct HipEngine::Impl {
         ah.list = cands.p;
         ah.cap = cap;
         ah.prune = hs_prune && !ps_fp16;
+        ah.cell_shift = hs_cell_shift;
         ah.pyr = pyr.p;
         ah.pyr_stride = hipk::hs_pyr_stride(ps_stride);
         return hipk::launch_harmonic_sum(ah, nb, stream);
@@ -622,6 +625,7 @@ int HipEngine::setup_impl(const SearchGeometry& g, const float* host_series, con
   if ((rc = d.buf.alloc(B * d.plan.M))) return rc;
   if ((rc = d.ps.alloc(B * d.ps_stride))) return rc;
   d.hs_prune = std::getenv("BRP_HS_FULL") == nullptr || std::atoi(std::getenv("BRP_HS_FULL")) == 0;
+  d.hs_cell_shift = (std::getenv("BRP_HS_CELL") && std::atoi(std::getenv("BRP_HS_CELL")) == 4) ? 2 : 3;
   if ((rc = d.pyr.alloc(B * hipk::hs_pyr_stride(d.ps_stride)))) return rc;
   if ((rc = d.partials.alloc(B * d.plan.wg1()))) return rc;
   if ((rc = d.delta.alloc(B))) return rc;

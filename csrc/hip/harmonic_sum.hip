@@ -177,46 +177,64 @@ __global__ void __launch_bounds__(kThreads) harmonic_sum_kernel(HSArgs a) {
 // bins a 16-index block touches gives an upper bound of every level value the
 // block owns; blocks whose bounds all stay at or below their thresholds emit
 // nothing and are skipped. Harmonics 4..16 take their maxima from 8-bin cells
-// (hs_cells_kernel), 1..3 from the spectrum: a wave's 64 blocks read ~1500
-// contiguous words instead of 16 x 1024 gathers. On the benchmark WU about
-// 2 % of the blocks pass (level 4; profiles/hs_prune_r2.txt); those are then
+// (hs_cells_kernel; 4-bin cells as a switch), 1..3 from the spectrum: a wave's
+// 64 blocks read ~1500 contiguous words instead of 16 x 1024 gathers. On the
+// benchmark spectrum at the chi^2 thresholds about 1.2 % of the blocks pass
+// (level 4; tools/experiments/hs_bound_sim.py, profiles/hs_bound_sim_r2.jsonl); those are then
 // computed exactly like harmonic_sum_kernel does, so the candidate lists are
 // the same (tests/test_gpu_kernels.py, bit for bit against the CPU model).
 constexpr int kBlk = 16;      // indices per block: one level-4 group
 constexpr int kBlkSpan = 20;  // + the 4-index reach of the level-1..3 groups whose first index lies in it
 constexpr int kWaveSpan = kWave * kBlk + (kBlkSpan - kBlk);  // indices a wave's 64 blocks reach
 
+// maxima of the spectrum over cells of 2^CK bins
+template <int CK>
 __global__ void __launch_bounds__(256) hs_cells_kernel(HSArgs a) {
+  constexpr int W = 1 << CK;
   const int b = blockIdx.y;
-  const uint32_t m = blockIdx.x * 256u + threadIdx.x;  // 8-bin cell
-  if (m >= hs_pyr_stride(a.ps_stride)) return;
+  const uint32_t m = blockIdx.x * 256u + threadIdx.x;
+  if (m >= (a.ps_stride >> CK) + 8) return;
   const float* P = a.ps + static_cast<size_t>(b) * a.ps_stride;
-  const uint32_t k0 = 8u * m;
-  float v[8];
-  if (k0 + 8 <= a.hhi) {
-    const float4 x = reinterpret_cast<const float4*>(P + k0)[0];
-    const float4 y = reinterpret_cast<const float4*>(P + k0)[1];
-    v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
-    v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
+  const uint32_t k0 = W * m;
+  float v[W];
+  if (k0 + W <= a.hhi) {
+#pragma unroll
+    for (int e = 0; e < W / 4; ++e) {
+      const float4 x = reinterpret_cast<const float4*>(P + k0)[e];
+      v[4 * e] = x.x; v[4 * e + 1] = x.y; v[4 * e + 2] = x.z; v[4 * e + 3] = x.w;
+    }
   } else {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = (k0 + e < a.hhi) ? P[k0 + e] : 0.0f;  // never read by the exact sums
+    for (int e = 0; e < W; ++e) v[e] = (k0 + e < a.hhi) ? P[k0 + e] : 0.0f;  // never read by the exact sums
   }
-  a.pyr[static_cast<size_t>(b) * a.pyr_stride + m] =
-      fmaxf(fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])), fmaxf(fmaxf(v[4], v[5]), fmaxf(v[6], v[7])));
+#pragma unroll
+  for (int w = W / 2; w >= 1; w /= 2)
+#pragma unroll
+    for (int e = 0; e < w; ++e) v[e] = fmaxf(v[e], v[e + w]);
+  a.pyr[static_cast<size_t>(b) * a.pyr_stride + m] = v[0];
 }
 
 // harmonics in the reference summation order, their source (0: spectrum,
-// 3: 8-bin cells) and their slice of a wave's staging buffer
+// CK: 2^CK-bin cells) and their slice of a wave's staging buffer
 constexpr int kHarm[16] = {16, 8, 12, 4, 14, 10, 6, 2, 15, 13, 11, 9, 7, 5, 3, 1};
-constexpr int hs_lvl(int l) { return l >= 4 ? 3 : 0; }
-constexpr int hs_wave_cells(int l) { return (((l * (kWaveSpan - 1) + 15) / 16) >> hs_lvl(l)) + 2; }
-constexpr int hs_slice(int q) {
-  int o = 0;
-  for (int r = 0; r < q; ++r) o += hs_wave_cells(kHarm[r]);
-  return o;
-}
-constexpr int kWaveCells = hs_slice(16);
+template <int CK>
+struct HsStage {
+  static constexpr int lvl(int l) { return l >= 4 ? CK : 0; }
+  static constexpr int wave_cells(int l) { return (((l * (kWaveSpan - 1) + 15) / 16) >> lvl(l)) + 2; }
+  static constexpr int slice(int q) {
+    int o = 0;
+    for (int r = 0; r < q; ++r) o += wave_cells(kHarm[r]);
+    return o;
+  }
+  static constexpr int kCells = slice(16);
+  static constexpr int chunks(int q) { return (wave_cells(kHarm[q]) + kWave - 1) / kWave; }
+  static constexpr int chunk0(int q) {
+    int o = 0;
+    for (int r = 0; r < q; ++r) o += chunks(r);
+    return o;
+  }
+  static constexpr int kLoads = chunk0(16);
+};
 
 __device__ __forceinline__ uint32_t hs_cell(int l, int k, int32_t i) {
   return (static_cast<uint32_t>(l * (i < 0 ? 0 : i) + 8) >> 4) >> k;
@@ -226,58 +244,86 @@ __device__ __forceinline__ uint32_t hs_cell(int l, int k, int32_t i) {
 // lane loads its words of all 16 slices first (unconditional, clamped
 // addresses: a guarded load per word made the compiler wait for each one
 // before its LDS write), then writes them to the wave's staging buffer
-constexpr int hs_chunks(int q) { return (hs_wave_cells(kHarm[q]) + kWave - 1) / kWave; }
-constexpr int hs_chunk0(int q) {
-  int o = 0;
-  for (int r = 0; r < q; ++r) o += hs_chunks(r);
-  return o;
-}
-constexpr int kStageLoads = hs_chunk0(16);
-
-template <int Q>
+template <int CK, int Q>
 __device__ __forceinline__ void hs_load(float* v, const float* P, const float* C8, uint32_t n8, uint32_t nps,
                                         int32_t I0, int lane) {
-  constexpr int L = kHarm[Q], K = hs_lvl(L);
+  using S = HsStage<CK>;
+  constexpr int L = kHarm[Q], K = S::lvl(L);
   const float* src = K ? C8 : P;
   const uint32_t lim = K ? n8 : nps;
   const uint32_t c0 = hs_cell(L, K, I0);
 #pragma unroll
-  for (int q = 0; q < hs_chunks(Q); ++q) {
+  for (int q = 0; q < S::chunks(Q); ++q) {
     const uint32_t c = c0 + static_cast<uint32_t>(lane + kWave * q);
     const float x = src[min(c, lim - 1)];
-    v[hs_chunk0(Q) + q] = c < lim ? x : 0.0f;
+    v[S::chunk0(Q) + q] = c < lim ? x : 0.0f;
   }
 }
 
-template <int Q>
+template <int CK, int Q>
 __device__ __forceinline__ void hs_store(float* buf, const float* v, int lane) {
-  constexpr int N = hs_wave_cells(kHarm[Q]);
+  using S = HsStage<CK>;
+  constexpr int N = S::wave_cells(kHarm[Q]);
 #pragma unroll
-  for (int q = 0; q < hs_chunks(Q); ++q) {
+  for (int q = 0; q < S::chunks(Q); ++q) {
     const int e = lane + kWave * q;
-    if (e < N) buf[hs_slice(Q) + e] = v[hs_chunk0(Q) + q];
+    if (e < N) buf[S::slice(Q) + e] = v[S::chunk0(Q) + q];
   }
 }
 
-// max of harmonic kHarm[Q] over the block [ib, ib + kBlkSpan) from the staged cells
-template <int Q>
-__device__ __forceinline__ float hs_block_max(const float* buf, int32_t I0, int32_t ib) {
-  constexpr int L = kHarm[Q], K = hs_lvl(L);
-  constexpr int kCells = (((L * (kBlkSpan - 1) + 15) / 16) >> K) + 2;
-  const float* s = buf + hs_slice(Q) - hs_cell(L, K, I0);
-  const uint32_t lo = hs_cell(L, K, ib), hi = hs_cell(L, K, ib + kBlkSpan - 1);
+// max of harmonic kHarm[Q] over the N indices [i, i + N) from the staged cells
+template <int CK, int Q, int N>
+__device__ __forceinline__ float hs_span_max(const float* buf, int32_t I0, int32_t i) {
+  using S = HsStage<CK>;
+  constexpr int L = kHarm[Q], K = S::lvl(L);
+  constexpr int kCells = (((L * (N - 1) + 15) / 16) >> K) + 2;
+  const float* s = buf + S::slice(Q) - hs_cell(L, K, I0);
+  const uint32_t lo = hs_cell(L, K, i), hi = hs_cell(L, K, i + N - 1);
   float m = s[lo];
 #pragma unroll
   for (int d = 1; d < kCells; ++d) m = fmaxf(m, s[min(lo + d, hi)]);
   return m;
 }
 
-template <int... Q>
+template <int CK, int... Q>
 __device__ __forceinline__ void hs_stage_all(std::integer_sequence<int, Q...>, float* buf, const float* P,
                                              const float* C8, uint32_t n8, uint32_t nps, int32_t I0, int lane) {
-  float v[kStageLoads];
-  (hs_load<Q>(v, P, C8, n8, nps, I0, lane), ...);
-  (hs_store<Q>(buf, v, lane), ...);
+  float v[HsStage<CK>::kLoads];
+  (hs_load<CK, Q>(v, P, C8, n8, nps, I0, lane), ...);
+  (hs_store<CK, Q>(buf, v, lane), ...);
+}
+
+// level bounds of block [ib, ib + 16) in the reference summation order (see
+// harmonic_sum_kernel). Level 4 owns one group, exactly the block's 16
+// indices; the groups of levels 1..3 whose first index lies in the block reach
+// 4 indices further, so their harmonics (the first 8) also take the max over
+// [ib + 16, ib + 20). (Measured on the benchmark spectrum with the chi^2
+// thresholds, tools/experiments/hs_bound_sim.py: level 4 decides almost every
+// flag; its own 16-index span halves the flagged blocks against one 20-index
+// span for all levels, 4-bin cells halve them again.)
+template <int CK, int... Q>
+__device__ __forceinline__ void hs_tail_max(std::integer_sequence<int, Q...>, const float* buf, int32_t I0, int32_t i,
+                                            float* m) {
+  ((m[Q] = fmaxf(m[Q], hs_span_max<CK, Q, kBlkSpan - kBlk>(buf, I0, i))), ...);
+}
+
+template <int CK, int... Q>
+__device__ __forceinline__ void hs_bounds(std::integer_sequence<int, Q...>, const float* buf, int32_t I0,
+                                          int32_t ib, float* u) {
+  const float m16[16] = {hs_span_max<CK, Q, kBlk>(buf, I0, ib)...};
+  float m20[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) m20[q] = m16[q];
+  hs_tail_max<CK>(std::make_integer_sequence<int, 8>{}, buf, I0, ib + kBlk, m20);
+  u[0] = m20[0];
+  u[1] = u[0] + m20[1];
+  u[2] = u[1] + (m20[2] + m20[3]);
+  u[3] = u[2] + (((m20[4] + m20[5]) + m20[6]) + m20[7]);
+  float v = m16[0];
+  v += m16[1];
+  v += m16[2] + m16[3];
+  v += ((m16[4] + m16[5]) + m16[6]) + m16[7];
+  u[4] = v + (((((((m16[8] + m16[9]) + m16[10]) + m16[11]) + m16[12]) + m16[13]) + m16[14]) + m16[15]);
 }
 
 // One thread per 16-index block computes the bounds; the wave then computes
@@ -286,10 +332,11 @@ __device__ __forceinline__ void hs_stage_all(std::integer_sequence<int, Q...>, f
 // of harmonic_sum_kernel for the groups whose first index lies in the block.
 // (No global block list: an atomic per wave on one counter serialised a first
 // version at 39 us.)
+template <int CK>
 __global__ void __launch_bounds__(256) hs_pruned_kernel(HSArgs a, uint32_t nblk) {
 #pragma clang fp contract(off)
   constexpr int kSubs = kWave / kBlkSpan;  // 3
-  __shared__ float stage[4][kWaveCells];
+  __shared__ float stage[4][HsStage<CK>::kCells];
   __shared__ float sv[4][kSubs][4][kBlkSpan];
   const int b = blockIdx.y;
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
@@ -301,8 +348,8 @@ __global__ void __launch_bounds__(256) hs_pruned_kernel(HSArgs a, uint32_t nblk)
   const int w2 = static_cast<int>(a.w2), fhi = static_cast<int>(a.fhi), hhi = static_cast<int>(a.hhi);
   const int32_t I0 = a.i_start + static_cast<int32_t>(kBlk * wave_blk0);
   float* buf = stage[wave];
-  hs_stage_all(std::make_integer_sequence<int, 16>{}, buf, P, a.pyr + static_cast<size_t>(b) * a.pyr_stride,
-               a.pyr_stride, a.ps_stride, I0, lane);
+  hs_stage_all<CK>(std::make_integer_sequence<int, 16>{}, buf, P, a.pyr + static_cast<size_t>(b) * a.pyr_stride,
+                   a.pyr_stride, a.ps_stride, I0, lane);
   // LDS operations of one wave complete in order; keep the compiler from moving them
   auto wave_sync = [] {
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
@@ -313,17 +360,8 @@ __global__ void __launch_bounds__(256) hs_pruned_kernel(HSArgs a, uint32_t nblk)
   bool flag = false;
   if (blk < nblk) {
     const int32_t ib = I0 + kBlk * lane;
-    // per-level bounds in the reference summation order (see harmonic_sum_kernel)
-    const float u0 = hs_block_max<0>(buf, I0, ib);
-    const float u1 = u0 + hs_block_max<1>(buf, I0, ib);
-    const float u2 = u1 + (hs_block_max<2>(buf, I0, ib) + hs_block_max<3>(buf, I0, ib));
-    const float u3 = u2 + (((hs_block_max<4>(buf, I0, ib) + hs_block_max<5>(buf, I0, ib)) +
-                            hs_block_max<6>(buf, I0, ib)) + hs_block_max<7>(buf, I0, ib));
-    const float u4 =
-        u3 + (((((((hs_block_max<8>(buf, I0, ib) + hs_block_max<9>(buf, I0, ib)) + hs_block_max<10>(buf, I0, ib)) +
-                  hs_block_max<11>(buf, I0, ib)) + hs_block_max<12>(buf, I0, ib)) + hs_block_max<13>(buf, I0, ib)) +
-               hs_block_max<14>(buf, I0, ib)) + hs_block_max<15>(buf, I0, ib));
-    const float u[5] = {u0, u1, u2, u3, u4};
+    float u[5];
+    hs_bounds<CK>(std::make_integer_sequence<int, 16>{}, buf, I0, ib, u);
 #pragma unroll
     for (int h = 0; h <= 4; ++h) {
       const int off = h ? 1 << (h - 1) : 0;
@@ -411,8 +449,14 @@ hipError_t launch_harmonic_sum(const HSArgs& a, int batch, hipStream_t s) {
   if (a.prune && a.mode == HS_F32) {
     const uint32_t nblk = hs_num_blocks(a.i_start, a.hhi);
     if (nblk == 0) return hipSuccess;
-    hipLaunchKernelGGL(hs_cells_kernel, dim3((hs_pyr_stride(a.ps_stride) + 255) / 256, batch), dim3(256), 0, s, a);
-    hipLaunchKernelGGL(hs_pruned_kernel, dim3((nblk + 255) / 256, batch), dim3(256), 0, s, a, nblk);
+    const dim3 gc((hs_pyr_stride(a.ps_stride) + 255) / 256, batch), gp((nblk + 255) / 256, batch);
+    if (a.cell_shift == 2) {
+      hipLaunchKernelGGL(hs_cells_kernel<2>, gc, dim3(256), 0, s, a);
+      hipLaunchKernelGGL(hs_pruned_kernel<2>, gp, dim3(256), 0, s, a, nblk);
+    } else {
+      hipLaunchKernelGGL(hs_cells_kernel<3>, gc, dim3(256), 0, s, a);
+      hipLaunchKernelGGL(hs_pruned_kernel<3>, gp, dim3(256), 0, s, a, nblk);
+    }
     return hipGetLastError();
   }
   const uint32_t tiles = hs_num_tiles(a.i_start, a.hhi);

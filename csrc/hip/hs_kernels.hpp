@@ -29,14 +29,16 @@ struct HSArgs {
   // exceed cap), list[1 + q] = (hs_pack(template, level, bin), power bits)
   uint2* list;
   uint32_t cap;
-  // pruned path (HS_F32): 8-bin maxima of the spectrum, [batch][pyr_stride]
+  // pruned path (HS_F32): maxima of the spectrum over cells of 2^cell_shift
+  // bins (2 or 3), [batch][pyr_stride]
   bool prune;
+  int cell_shift;
   float* pyr;
   uint32_t pyr_stride;
 };
 
-// 8-bin cells covering the spectrum row (bins >= hhi count as 0)
-__host__ __device__ constexpr uint32_t hs_pyr_stride(uint32_t ps_stride) { return ps_stride / 8 + 8; }
+// cells covering the spectrum row, room for 4-bin cells (bins >= hhi count as 0)
+__host__ __device__ constexpr uint32_t hs_pyr_stride(uint32_t ps_stride) { return ps_stride / 4 + 8; }
 // 16-bin blocks of the pruned path (tile grid of kHsTile, i_start == 8 mod 16)
 uint32_t hs_num_blocks(int32_t i_start, uint32_t hhi);
 

@@ -86,14 +86,20 @@ def test_harmonic_sum_matches_cpu_bitwise(brp, gpu, tmp_path, monkeypatch, windo
         np.testing.assert_array_equal(pw_g, pw_c)
 
 
-@pytest.mark.parametrize("full,thr", [("0", (9.0, 12.0, 16.0, 22.0, 33.0)), ("1", (9.0, 12.0, 16.0, 22.0, 33.0)),
-                                      ("0", (11.0, 12.5, 15.5, 21.0, 31.0)), ("0", (13.0, 15.0, 18.0, 24.0, 34.5))])
-def test_harmonic_sum_bench_size_matches_cpu_bitwise(brp, gpu, monkeypatch, full, thr):
+@pytest.mark.parametrize("full,thr,cell", [("0", (9.0, 12.0, 16.0, 22.0, 33.0), "8"),
+                                           ("1", (9.0, 12.0, 16.0, 22.0, 33.0), "8"),
+                                           ("0", (11.0, 12.5, 15.5, 21.0, 31.0), "8"),
+                                           ("0", (13.0, 15.0, 18.0, 24.0, 34.5), "8"),
+                                           ("0", (11.0, 12.5, 15.5, 21.0, 31.0), "4"),
+                                           ("0", (18.139, 21.241, 26.269, 34.648, 48.958), "8")])
+def test_harmonic_sum_bench_size_matches_cpu_bitwise(brp, gpu, monkeypatch, full, thr, cell):
     """Benchmark geometry (hhi = 5.27 M bins, two templates of a batch): the
     harmonic-sum candidates equal the CPU model's on the same spectrum, for the
-    pruned path at thresholds that flag many / some / few blocks and for the
-    full gather kernel."""
+    pruned path at thresholds that flag many / some / few blocks (down to the
+    search's chi^2 levels), with 8-bin (default) and 4-bin bound cells, and for
+    the full gather kernel."""
     monkeypatch.setenv("BRP_HS_FULL", full)
+    monkeypatch.setenv("BRP_HS_CELL", cell)
     hdr, series, _ = brp.read_work_unit(str(WU))
     opt = dict(OPT_BENCH, white=True)
     geom = brp.derive_geometry(hdr, opt)
@@ -105,7 +111,7 @@ def test_harmonic_sum_bench_size_matches_cpu_bitwise(brp, gpu, monkeypatch, full
     for k in range(2):
         ps_gpu, _ = eng.power_spectrum(float(np.float32(P[k])), float(np.float32(tau[k])), float(np.float32(psi[k])))
         ref, _ = brp.cpu_harmonic_sum(ps_gpu, geom, thr)
-        assert sum(len(ref[h][0]) for h in range(5)) > 0
+        assert sum(len(ref[h][0]) for h in range(5)) > 0 or thr[0] > 18.0
         for h in range(5):
             assert len(ref[h][0]) > 0 or thr[0] > 10.0
             np.testing.assert_array_equal(outs[k][h][0], ref[h][0])
