@@ -447,6 +447,7 @@ PYBIND11_MODULE(_brp, m) {
              }
              return cands_to_list(out);
            })
+      .def("set_ps_fp16", [](HipEngine& e, bool on) { e.set_ps_fp16(on); })
       .def("adopt_series", [](HipEngine& e, const HipEngine& src) { check(e.adopt_series(src), "HipEngine.adopt_series"); })
       .def("power_spectrum",
            [](HipEngine& e, float P, float tau, float psi) {

@@ -408,7 +408,7 @@ struct HipEngine::Impl {
         ah.thr = thr.p;
         ah.list = cands.p;
         ah.cap = cap;
-        ah.prune = hs_prune && !ps_fp16;
+        ah.prune = hs_prune;
         ah.cell_shift = hs_cell_shift;
         ah.pyr = pyr.p;
         ah.pyr_stride = hipk::hs_pyr_stride(ps_stride);

@@ -14,6 +14,7 @@
 // dirty-page flags that the host then scans, each workgroup appends only the
 // (bin, power) pairs above the device threshold to per-level candidate lists
 // (wave-aggregated atomics); the host merges them into the candidate table.
+#include <type_traits>
 #include <utility>
 
 #include "hip_common.hpp"
@@ -187,25 +188,47 @@ constexpr int kBlk = 16;      // indices per block: one level-4 group
 constexpr int kBlkSpan = 20;  // + the 4-index reach of the level-1..3 groups whose first index lies in it
 constexpr int kWaveSpan = kWave * kBlk + (kBlkSpan - kBlk);  // indices a wave's 64 blocks reach
 
-// maxima of the spectrum over cells of 2^CK bins
-template <int CK>
+// spectrum element type of a mode (HS_F16: fp16 spectrum, widened exactly)
+template <int MODE>
+using PsT = std::conditional_t<MODE == HS_F32, float, _Float16>;
+template <int MODE>
+__device__ __forceinline__ const PsT<MODE>* ps_row(const HSArgs& a, int b) {
+  if constexpr (MODE == HS_F32) return a.ps + static_cast<size_t>(b) * a.ps_stride;
+  else return a.ps16 + static_cast<size_t>(b) * a.ps_stride;
+}
+
+// maxima of the spectrum over cells of 2^CK bins (fp32 cells for either spectrum)
+template <int CK, int MODE>
 __global__ void __launch_bounds__(256) hs_cells_kernel(HSArgs a) {
   constexpr int W = 1 << CK;
   const int b = blockIdx.y;
   const uint32_t m = blockIdx.x * 256u + threadIdx.x;
   if (m >= (a.ps_stride >> CK) + 8) return;
-  const float* P = a.ps + static_cast<size_t>(b) * a.ps_stride;
+  const PsT<MODE>* P = ps_row<MODE>(a, b);
   const uint32_t k0 = W * m;
   float v[W];
   if (k0 + W <= a.hhi) {
+    if constexpr (MODE == HS_F32) {
 #pragma unroll
-    for (int e = 0; e < W / 4; ++e) {
-      const float4 x = reinterpret_cast<const float4*>(P + k0)[e];
-      v[4 * e] = x.x; v[4 * e + 1] = x.y; v[4 * e + 2] = x.z; v[4 * e + 3] = x.w;
+      for (int e = 0; e < W / 4; ++e) {
+        const float4 x = reinterpret_cast<const float4*>(P + k0)[e];
+        v[4 * e] = x.x; v[4 * e + 1] = x.y; v[4 * e + 2] = x.z; v[4 * e + 3] = x.w;
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < W / 4; ++e) {  // 4 halves per 8-byte load
+        const uint2 x = reinterpret_cast<const uint2*>(P + k0)[e];
+        const uint32_t w[2] = {x.x, x.y};
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          v[4 * e + q] = static_cast<float>(
+              __builtin_bit_cast(_Float16, static_cast<unsigned short>(w[q / 2] >> (16 * (q % 2)))));
+      }
     }
   } else {
 #pragma unroll
-    for (int e = 0; e < W; ++e) v[e] = (k0 + e < a.hhi) ? P[k0 + e] : 0.0f;  // never read by the exact sums
+    for (int e = 0; e < W; ++e)  // never read by the exact sums
+      v[e] = (k0 + e < a.hhi) ? static_cast<float>(P[k0 + e]) : 0.0f;
   }
 #pragma unroll
   for (int w = W / 2; w >= 1; w /= 2)
@@ -244,18 +267,17 @@ __device__ __forceinline__ uint32_t hs_cell(int l, int k, int32_t i) {
 // lane loads its words of all 16 slices first (unconditional, clamped
 // addresses: a guarded load per word made the compiler wait for each one
 // before its LDS write), then writes them to the wave's staging buffer
-template <int CK, int Q>
-__device__ __forceinline__ void hs_load(float* v, const float* P, const float* C8, uint32_t n8, uint32_t nps,
+template <int CK, int Q, typename T>
+__device__ __forceinline__ void hs_load(float* v, const T* P, const float* C8, uint32_t n8, uint32_t nps,
                                         int32_t I0, int lane) {
   using S = HsStage<CK>;
   constexpr int L = kHarm[Q], K = S::lvl(L);
-  const float* src = K ? C8 : P;
   const uint32_t lim = K ? n8 : nps;
   const uint32_t c0 = hs_cell(L, K, I0);
 #pragma unroll
   for (int q = 0; q < S::chunks(Q); ++q) {
     const uint32_t c = c0 + static_cast<uint32_t>(lane + kWave * q);
-    const float x = src[min(c, lim - 1)];
+    const float x = K ? C8[min(c, lim - 1)] : static_cast<float>(P[min(c, lim - 1)]);
     v[S::chunk0(Q) + q] = c < lim ? x : 0.0f;
   }
 }
@@ -285,8 +307,8 @@ __device__ __forceinline__ float hs_span_max(const float* buf, int32_t I0, int32
   return m;
 }
 
-template <int CK, int... Q>
-__device__ __forceinline__ void hs_stage_all(std::integer_sequence<int, Q...>, float* buf, const float* P,
+template <int CK, typename T, int... Q>
+__device__ __forceinline__ void hs_stage_all(std::integer_sequence<int, Q...>, float* buf, const T* P,
                                              const float* C8, uint32_t n8, uint32_t nps, int32_t I0, int lane) {
   float v[HsStage<CK>::kLoads];
   (hs_load<CK, Q>(v, P, C8, n8, nps, I0, lane), ...);
@@ -332,7 +354,7 @@ __device__ __forceinline__ void hs_bounds(std::integer_sequence<int, Q...>, cons
 // of harmonic_sum_kernel for the groups whose first index lies in the block.
 // (No global block list: an atomic per wave on one counter serialised a first
 // version at 39 us.)
-template <int CK>
+template <int CK, int MODE>
 __global__ void __launch_bounds__(256) hs_pruned_kernel(HSArgs a, uint32_t nblk) {
 #pragma clang fp contract(off)
   constexpr int kSubs = kWave / kBlkSpan;  // 3
@@ -343,7 +365,7 @@ __global__ void __launch_bounds__(256) hs_pruned_kernel(HSArgs a, uint32_t nblk)
   const uint32_t wave_blk0 = blockIdx.x * 256u + static_cast<uint32_t>(wave * kWave);
   if (wave_blk0 >= nblk) return;  // whole wave
   const uint32_t blk = wave_blk0 + lane;
-  const float* P = a.ps + static_cast<size_t>(b) * a.ps_stride;
+  const PsT<MODE>* P = ps_row<MODE>(a, b);
   const float* thr = a.thr + static_cast<size_t>(b) * kHsThrStride;
   const int w2 = static_cast<int>(a.w2), fhi = static_cast<int>(a.fhi), hhi = static_cast<int>(a.hhi);
   const int32_t I0 = a.i_start + static_cast<int32_t>(kBlk * wave_blk0);
@@ -390,7 +412,7 @@ __global__ void __launch_bounds__(256) hs_pruned_kernel(HSArgs a, uint32_t nblk)
     const int i = ib + li;
     float s1 = ninf, s2 = ninf, s3 = ninf, s4 = ninf, p0 = 0.0f;
     if (act && i >= w2 && i < hhi) {
-      auto ld = [&](int l) { return P[(l * i + 8) >> 4]; };
+      auto ld = [&](int l) { return static_cast<float>(P[(l * i + 8) >> 4]); };
       float sum = ld(16);
       p0 = sum;
       sum += ld(8);
@@ -446,17 +468,23 @@ uint32_t hs_num_tiles(int32_t i_start, uint32_t hhi) {
 }
 
 hipError_t launch_harmonic_sum(const HSArgs& a, int batch, hipStream_t s) {
-  if (a.prune && a.mode == HS_F32) {
+  if (a.prune) {
     const uint32_t nblk = hs_num_blocks(a.i_start, a.hhi);
     if (nblk == 0) return hipSuccess;
     const dim3 gc((hs_pyr_stride(a.ps_stride) + 255) / 256, batch), gp((nblk + 255) / 256, batch);
-    if (a.cell_shift == 2) {
-      hipLaunchKernelGGL(hs_cells_kernel<2>, gc, dim3(256), 0, s, a);
-      hipLaunchKernelGGL(hs_pruned_kernel<2>, gp, dim3(256), 0, s, a, nblk);
+#define BRP_HS_PRUNED(CK, MODE)                                              \
+  do {                                                                      \
+    hipLaunchKernelGGL((hs_cells_kernel<CK, MODE>), gc, dim3(256), 0, s, a); \
+    hipLaunchKernelGGL((hs_pruned_kernel<CK, MODE>), gp, dim3(256), 0, s, a, nblk); \
+  } while (0)
+    if (a.mode == HS_F16) {
+      if (a.cell_shift == 2) BRP_HS_PRUNED(2, HS_F16);
+      else BRP_HS_PRUNED(3, HS_F16);
     } else {
-      hipLaunchKernelGGL(hs_cells_kernel<3>, gc, dim3(256), 0, s, a);
-      hipLaunchKernelGGL(hs_pruned_kernel<3>, gp, dim3(256), 0, s, a, nblk);
+      if (a.cell_shift == 2) BRP_HS_PRUNED(2, HS_F32);
+      else BRP_HS_PRUNED(3, HS_F32);
     }
+#undef BRP_HS_PRUNED
     return hipGetLastError();
   }
   const uint32_t tiles = hs_num_tiles(a.i_start, a.hhi);

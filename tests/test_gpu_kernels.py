@@ -118,6 +118,31 @@ def test_harmonic_sum_bench_size_matches_cpu_bitwise(brp, gpu, monkeypatch, full
             np.testing.assert_array_equal(outs[k][h][1], ref[h][1])
 
 
+@pytest.mark.parametrize("thr", [(9.0, 12.0, 16.0, 22.0, 33.0), (18.139, 21.241, 26.269, 34.648, 48.958)])
+def test_harmonic_sum_fp16_pruned_equals_full(brp, gpu, monkeypatch, thr):
+    """Config 5 (fp16 spectrum): the pruned harmonic sum (bounds from fp32 cell
+    maxima of the fp16 spectrum, exact sums widened to fp32) gives the
+    candidate lists of the full fp16 gather kernel bit for bit, on the
+    benchmark geometry."""
+    hdr, series, _ = brp.read_work_unit(str(WU))
+    opt = dict(OPT_BENCH, white=True)
+    geom = brp.derive_geometry(hdr, opt)
+    P, tau, psi = brp.read_template_bank(str(BANK))
+    outs = {}
+    for full in ("0", "1"):
+        monkeypatch.setenv("BRP_HS_FULL", full)
+        eng = _engine(brp, geom, series, batch=2)
+        eng.set_ps_fp16(True)
+        eng.whiten(opt, brp.read_zaplist(str(ZAP)), series)
+        outs[full] = eng.process(P[:2].astype(np.float32), tau[:2].astype(np.float32), psi[:2].astype(np.float32),
+                                 list(thr))
+    assert sum(len(outs["1"][k][h][0]) for k in range(2) for h in range(5)) > 0 or thr[0] > 18.0
+    for k in range(2):
+        for h in range(5):
+            np.testing.assert_array_equal(outs["0"][k][h][0], outs["1"][k][h][0])
+            np.testing.assert_array_equal(outs["0"][k][h][1], outs["1"][k][h][1])
+
+
 def test_whitening_wide_window_matches_cpu(brp, gpu, tmp_path):
     """-B above the LDS kernel's 3072: whitening stays on the device (wide
     running median) and matches the CPU whitening."""
