@@ -1076,13 +1076,18 @@ int HipEngine::benchmark_stages(const TemplateInput* t, int n, int reps, std::ve
   if (!d.ready) return RADPUL_EMISC;
   const int nb = std::min(n, d.batch);
   const SearchGeometry& g = d.g;
+  // BRP_STAGE_THR_SCALE: scale the chi^2 thresholds (harmonic-sum ablations:
+  // a large factor leaves the pruned kernel no exact work)
+  const char* ts = std::getenv("BRP_STAGE_THR_SCALE");
+  const float thr_scale = ts ? static_cast<float>(std::atof(ts)) : 1.0f;
   for (int k = 0; k < nb; ++k) {
     TemplateDev td{};
     td.p = make_resamp_params(g.nsamples, g.n_unpadded, g.fft_size, g.dt, g.step_inv, t[k].P, t[k].tau, t[k].Psi0);
     td.n_steps = resamp_n_steps(td.p, kSinLut, kCosLut);
     td.mu0 = d.mu0s[0];
     d.h_tmpl.p[k] = td;
-    for (int h = 0; h < kNumHarmonicLevels; ++h) d.h_thr.p[k * hipk::kHsThrStride + h] = d.g.chi2_thr[h];
+    for (int h = 0; h < kNumHarmonicLevels; ++h)
+      d.h_thr.p[k * hipk::kHsThrStride + h] = d.g.chi2_thr[h] * thr_scale;
   }
   std::atomic_thread_fence(std::memory_order_seq_cst);
   BRP_HIP_CHECK(d.enqueue(nb), RADPUL_HIP_KERNEL_INVOKE);
