@@ -5,6 +5,7 @@
 #include <chrono>
 #include <cmath>
 #include <condition_variable>
+#include <deque>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -326,30 +327,52 @@ int SearchSession::run(uint32_t begin, uint32_t end, CandidateTable& table, Sear
   table.thresholds(g.chi2_thr, thr_shared);
   std::atomic<uint32_t> next_first{begin};
   std::atomic<bool> stop{false};
+  // Each worker keeps up to max_in_flight() batches of its backend submitted
+  // (the next batch is launched while the previous one runs), completing them
+  // in submission order.
   auto worker = [&](Backend* be) {
-    for (;;) {
-      // a suspended task starts no GPU work; batches already launched
-      // finish inside their critical section (demod_binary.c:1241-1296)
-      boinc::suspend_point();
-      if (stop.load()) return;
-      const uint32_t first = next_first.fetch_add(static_cast<uint32_t>(B));
-      if (first >= end) return;
-      const int n = static_cast<int>(std::min<uint32_t>(B, end - first));
-      float thr[kNumHarmonicLevels];
+    const int depth = std::max(1, be->max_in_flight());
+    std::deque<uint32_t> inflight;  // first template of each submitted batch
+    auto publish = [&](BatchResult&& br) {
       {
         std::lock_guard<std::mutex> lk(mu);
-        std::memcpy(thr, thr_shared, sizeof(thr));
-      }
-      BatchResult br;
-      br.first = first;
-      boinc::begin_critical_section();
-      br.rc = be->process(&d.tin[first], n, thr, br.cands);
-      boinc::end_critical_section();
-      {
-        std::lock_guard<std::mutex> lk(mu);
-        ready.emplace(first, std::move(br));
+        ready.emplace(br.first, std::move(br));
       }
       cv.notify_all();
+    };
+    for (;;) {
+      while (static_cast<int>(inflight.size()) < depth) {
+        // a suspended task starts no GPU work; batches already launched
+        // finish inside their critical section (demod_binary.c:1241-1296)
+        boinc::suspend_point();
+        if (stop.load()) break;
+        const uint32_t first = next_first.fetch_add(static_cast<uint32_t>(B));
+        if (first >= end) break;
+        const int n = static_cast<int>(std::min<uint32_t>(B, end - first));
+        float thr[kNumHarmonicLevels];
+        {
+          std::lock_guard<std::mutex> lk(mu);
+          std::memcpy(thr, thr_shared, sizeof(thr));
+        }
+        boinc::begin_critical_section();
+        const int rc = be->submit(&d.tin[first], n, thr);
+        if (rc) {
+          boinc::end_critical_section();
+          BatchResult br;
+          br.first = first;
+          br.rc = rc;
+          publish(std::move(br));
+          continue;
+        }
+        inflight.push_back(first);
+      }
+      if (inflight.empty()) return;
+      BatchResult br;
+      br.first = inflight.front();
+      inflight.pop_front();
+      br.rc = be->complete(br.cands);
+      boinc::end_critical_section();
+      publish(std::move(br));
     }
   };
   std::vector<std::thread> threads;

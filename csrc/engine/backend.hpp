@@ -5,6 +5,7 @@
 // template; the driver applies them to the candidate table in template order.
 #pragma once
 
+#include <deque>
 #include <memory>
 #include <string>
 #include <vector>
@@ -61,6 +62,33 @@ class Backend {
   virtual int preferred_batch() const = 0;
   virtual int device() const { return -1; }
   virtual BackendStats stats() const { return {}; }
+  // Pipelined form of process(): up to max_in_flight() batches submitted
+  // before the oldest is completed; complete() returns results in submission
+  // order. The default queues the arguments and runs process() inside
+  // complete() (the HIP backend launches at submit()).
+  virtual int max_in_flight() const { return 1; }
+  virtual int submit(const TemplateInput* t, int n, const float thr[kNumHarmonicLevels]) {
+    Pending p;
+    p.t = t;
+    p.n = n;
+    for (int h = 0; h < kNumHarmonicLevels; ++h) p.thr[h] = thr[h];
+    pending_.push_back(p);
+    return 0;
+  }
+  virtual int complete(std::vector<TemplateCands>& out) {
+    if (pending_.empty()) return -1;
+    const Pending p = pending_.front();
+    pending_.pop_front();
+    return process(p.t, p.n, p.thr, out);
+  }
+
+ private:
+  struct Pending {
+    const TemplateInput* t;
+    int n;
+    float thr[kNumHarmonicLevels];
+  };
+  std::deque<Pending> pending_;
 };
 
 std::unique_ptr<Backend> make_cpu_backend();

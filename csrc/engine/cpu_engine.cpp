@@ -40,6 +40,9 @@ class CpuEngine final : public Backend {
     return 0;
   }
   int preferred_batch() const override { return 1; }
+  // queued submit/complete (Backend defaults), two deep: the search workers'
+  // pipelined loop runs on the CPU golden model too
+  int max_in_flight() const override { return 2; }
   BackendStats stats() const override { return stats_; }
 
  private:
@@ -88,6 +91,7 @@ class ReplayEngine final : public Backend {
     return 0;
   }
   int preferred_batch() const override { return batch_; }
+  int max_in_flight() const override { return 2; }  // as the HIP pipelines
   BackendStats stats() const override { return stats_; }
 
  private:

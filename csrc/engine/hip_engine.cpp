@@ -192,7 +192,7 @@ std::vector<float2> stage_table(uint32_t L) {
 struct HipEngine::Impl {
   int device = 0;
   hipStream_t stream = nullptr;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;  // views of the current batch I/O slot
   int batch = 4;
   uint32_t cap = 1u << 20;      // candidate slots per batch (all templates and levels)
   uint32_t kcopy = 1024;        // slots copied back with every batch (more: second copy)
@@ -246,11 +246,47 @@ struct HipEngine::Impl {
                                 // 44 KB LDS / 125 VGPRs per workgroup: 16.4-16.7k vs 15.6-15.8k templates/s)
   DevBuf<double> partials;      // [batch][wg1]
   DevBuf<double> delta;         // [batch] mean-padding correction
-  // per-batch input, ONE host->device copy: thresholds | templates
-  DevBuf<uint8_t> in;
-  struct { TemplateDev* p = nullptr; } tmpl;  // views into `in`
+  // Per-batch I/O, double-buffered so that a pipeline can keep two batches in
+  // flight on its stream (submit / complete): the next batch's parameters are
+  // written and its graph launched while the previous one runs, so the GPU
+  // does not wait on the host between batches. The FFT, spectrum and cell
+  // buffers stay single: the stream orders the two batches.
+  //   in:    thresholds | templates (ONE host->device copy, or written in place)
+  //   cands: [1 + cap] count | (packed key, power) entries
+  struct BatchIO {
+    DevBuf<uint8_t> in;
+    PinnedBuf<uint8_t> h_in;
+    DevBuf<uint2> cands;
+    PinnedBuf<uint2> h_cands;
+    uint8_t* h_in_p = nullptr;  // host view of the parameters (pinned copy or `in` itself)
+    uint2* h_cands_p = nullptr;  // host view of the results (pinned copy or `cands` itself)
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    int nb = 0;
+    bool pending = false;
+  };
+  static constexpr int kIoSlots = 2;
+  BatchIO io[kIoSlots];
+  int io_cur = 0, io_next = 0, io_head = 0;
+  // views of slot io_cur, used by enqueue_stage / capture and the test hooks
+  struct { uint8_t* p = nullptr; } in, h_in;
+  struct { TemplateDev* p = nullptr; } tmpl;
   struct { float* p = nullptr; } thr;
-  DevBuf<uint2> cands;          // [1 + cap]: count | (packed key, power) entries
+  struct { uint2* p = nullptr; } cands;
+  void select_io(int i) {
+    io_cur = i;
+    BatchIO& o = io[i];
+    in.p = o.in.p;
+    h_in.p = o.h_in_p;
+    thr.p = reinterpret_cast<float*>(o.in.p);
+    tmpl.p = reinterpret_cast<TemplateDev*>(o.in.p + thr_bytes);
+    h_thr.p = reinterpret_cast<float*>(o.h_in_p);
+    h_tmpl.p = reinterpret_cast<TemplateDev*>(o.h_in_p + thr_bytes);
+    cands.p = o.cands.p;
+    h_cands.p = o.h_cands_p;
+    ev0 = o.ev0;
+    ev1 = o.ev1;
+  }
+  bool io_busy() const { return io[0].pending || io[1].pending; }
   DevBuf<float2> tw_hi, tw_lo;
   DevBuf<float2> w_spec, w_z;   // whitening scratch: half spectrum, packed inverse input
   DevBuf<float> w_psw, w_med;   // whitening scratch: power spectrum, running median
@@ -258,15 +294,14 @@ struct HipEngine::Impl {
   DevBuf<float2> w_znoise;
   DevBuf<float2> t_st1, t_st2, t_st3, t_p1, t_p2col, t_p2lo, t_p2hi, t_p3;
 
-  PinnedBuf<uint8_t> h_in;
   struct { TemplateDev* p = nullptr; } h_tmpl;
   struct { float* p = nullptr; } h_thr;
-  PinnedBuf<uint2> h_cands;     // [1 + kcopy]
+  struct { uint2* p = nullptr; } h_cands;  // [1 + kcopy]
   size_t thr_bytes = 64;        // thresholds area at the start of `in`: [batch][kHsThrStride] floats
   uint32_t slots = 1;           // work-unit slots of the series buffer (multi-WU batching)
   std::vector<float> mu0s;      // per-slot padding offset
 
-  std::map<int, hipGraphExec_t> graphs;
+  std::map<int, hipGraphExec_t> graphs;  // key: batch size * kIoSlots + I/O slot
   BackendStats st;
 
   hipk::FFTTables tables() const {
@@ -331,8 +366,10 @@ struct HipEngine::Impl {
   ~Impl() {
     bump_series();  // readers of this series must not launch any more
     for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second);
-    if (ev0) (void)hipEventDestroy(ev0);
-    if (ev1) (void)hipEventDestroy(ev1);
+    for (BatchIO& o : io) {
+      if (o.ev0) (void)hipEventDestroy(o.ev0);
+      if (o.ev1) (void)hipEventDestroy(o.ev1);
+    }
     if (stream) (void)hipStreamDestroy(stream);
   }
 
@@ -532,8 +569,11 @@ int HipEngine::init(int device, int batch) {
   impl_->device = device;
   impl_->batch = batch > 0 ? batch : 4;
   BRP_HIP_CHECK(hipStreamCreateWithFlags(&impl_->stream, hipStreamNonBlocking), RADPUL_HIP_DEVICE_SET);
-  BRP_HIP_CHECK(hipEventCreate(&impl_->ev0), RADPUL_HIP_DEVICE_SET);
-  BRP_HIP_CHECK(hipEventCreate(&impl_->ev1), RADPUL_HIP_DEVICE_SET);
+  for (auto& o : impl_->io) {
+    BRP_HIP_CHECK(hipEventCreate(&o.ev0), RADPUL_HIP_DEVICE_SET);
+    BRP_HIP_CHECK(hipEventCreate(&o.ev1), RADPUL_HIP_DEVICE_SET);
+  }
+  impl_->select_io(0);
   hipDeviceProp_t prop;
   BRP_HIP_CHECK(hipGetDeviceProperties(&prop, device), RADPUL_HIP_DEVICE_PROP);
   log_message(LOG_INFO, true, "Using HIP device #%d: %s (%s, %d CUs, %.1f GB)\n", device, prop.name,
@@ -644,35 +684,41 @@ int HipEngine::setup_impl(const SearchGeometry& g, const float* host_series, con
     d.fg_in = f.empty() || f == "in" || f == "both" || f == "1";
     d.fg_out = f == "out" || f == "both" || f == "1";
   }
-  if ((rc = d.in.alloc(in_bytes, d.fg_in))) return rc;
-  uint8_t* in_host = d.fg_in ? static_cast<uint8_t*>(host_view(d.device, d.in.p, in_bytes)) : nullptr;
-  if (d.fg_in && in_host == nullptr) {
-    log_message(LOG_WARN, true, "Fine-grained device memory is not host visible; copying the batch parameters.\n");
-    d.fg_in = false;
-    if ((rc = d.in.alloc(in_bytes))) return rc;
+  for (int i = 0; i < Impl::kIoSlots; ++i) {
+    Impl::BatchIO& o = d.io[i];
+    o.pending = false;
+    if ((rc = o.in.alloc(in_bytes, d.fg_in))) return rc;
+    uint8_t* in_host = d.fg_in ? static_cast<uint8_t*>(host_view(d.device, o.in.p, in_bytes)) : nullptr;
+    if (d.fg_in && in_host == nullptr) {
+      log_message(LOG_WARN, true, "Fine-grained device memory is not host visible; copying the batch parameters.\n");
+      d.fg_in = false;
+      if ((rc = o.in.alloc(in_bytes))) return rc;
+      if (i > 0) return RADPUL_EMEM;  // slot 0 was host visible: inconsistent
+    }
+    if ((rc = o.cands.alloc(1 + d.cap, d.fg_out))) return rc;
+    if (d.fg_in) {
+      o.h_in_p = in_host;
+    } else {
+      if ((rc = o.h_in.alloc(in_bytes))) return rc;
+      o.h_in_p = o.h_in.p;
+    }
+    uint2* cands_host =
+        d.fg_out ? static_cast<uint2*>(host_view(d.device, o.cands.p, sizeof(uint2) * (1 + d.kcopy))) : nullptr;
+    if (d.fg_out && cands_host == nullptr) {
+      log_message(LOG_WARN, true, "Fine-grained device memory is not host visible; copying the results.\n");
+      d.fg_out = false;
+      if ((rc = o.cands.alloc(1 + d.cap))) return rc;
+      if (i > 0) return RADPUL_EMEM;
+    }
+    if (d.fg_out) {
+      o.h_cands_p = cands_host;  // non-owning view
+    } else {
+      if ((rc = o.h_cands.alloc(1 + d.kcopy))) return rc;
+      o.h_cands_p = o.h_cands.p;
+    }
   }
-  d.thr.p = reinterpret_cast<float*>(d.in.p);
-  d.tmpl.p = reinterpret_cast<TemplateDev*>(d.in.p + d.thr_bytes);
-  if ((rc = d.cands.alloc(1 + d.cap, d.fg_out))) return rc;
-  if (d.fg_in) {
-    d.h_thr.p = reinterpret_cast<float*>(in_host);
-    d.h_tmpl.p = reinterpret_cast<TemplateDev*>(in_host + d.thr_bytes);
-  } else {
-    if ((rc = d.h_in.alloc(in_bytes))) return rc;
-    d.h_thr.p = reinterpret_cast<float*>(d.h_in.p);
-    d.h_tmpl.p = reinterpret_cast<TemplateDev*>(d.h_in.p + d.thr_bytes);
-  }
-  uint2* cands_host = d.fg_out ? static_cast<uint2*>(host_view(d.device, d.cands.p, sizeof(uint2) * (1 + d.kcopy))) : nullptr;
-  if (d.fg_out && cands_host == nullptr) {
-    log_message(LOG_WARN, true, "Fine-grained device memory is not host visible; copying the results.\n");
-    d.fg_out = false;
-    if ((rc = d.cands.alloc(1 + d.cap))) return rc;
-  }
-  if (d.fg_out) {
-    d.h_cands.p = cands_host;  // non-owning view (PinnedBuf::n stays 0)
-  } else if ((rc = d.h_cands.alloc(1 + d.kcopy))) {
-    return rc;
-  }
+  d.io_next = d.io_head = 0;
+  d.select_io(0);
   std::vector<float2> hi, lo;
   build_twiddles(4ull * d.plan.M, hi, lo);
   if ((rc = d.tw_hi.alloc(hi.size()))) return rc;
@@ -906,109 +952,141 @@ int HipEngine::process(const TemplateInput* t, int n, const float thr[kNumHarmon
 int HipEngine::process(const TemplateInput* t, int n, const float* thr, int thr_stride,
                        std::vector<TemplateCands>& out) {
   Impl& d = *impl_;
-  if (!d.ready) return RADPUL_EMISC;
+  if (d.io_busy()) return RADPUL_EMISC;  // submitted batches must be completed first
+  out.clear();
+  out.resize(n);
+  std::vector<TemplateCands> part;
+  for (int off = 0; off < n; off += d.batch) {
+    const int nb = std::min(d.batch, n - off);
+    int rc = submit(t + off, nb, thr + static_cast<size_t>(off) * thr_stride, thr_stride);
+    if (rc == 0) rc = complete(part);
+    if (rc) return rc;
+    for (int k = 0; k < nb; ++k) out[off + k] = std::move(part[k]);
+  }
+  return 0;
+}
+
+int HipEngine::max_in_flight() const { return Impl::kIoSlots; }
+
+int HipEngine::submit(const TemplateInput* t, int nb, const float* thr, int thr_stride) {
+  Impl& d = *impl_;
+  if (!d.ready || nb < 1 || nb > d.batch) return RADPUL_EMISC;
   if (!d.shared_series_valid()) {
     log_message(LOG_ERROR, true, "Pipeline reads a whitened series that was rewritten or freed since it was adopted.\n");
     return RADPUL_EVAL;
   }
+  const int slot = d.io_next;
+  if (d.io[slot].pending) return RADPUL_EMISC;  // more than kIoSlots batches in flight
   BRP_HIP_CHECK(hipSetDevice(d.device), RADPUL_HIP_DEVICE_SET);  // worker threads drive their own device
-  out.clear();
-  out.resize(n);
   const SearchGeometry& g = d.g;
-  for (int off = 0; off < n; off += d.batch) {
-    const int nb = std::min(d.batch, n - off);
-    {
-      trace::Range launch("brp:batch_launch");
-      for (int k = 0; k < nb; ++k) {
-        TemplateDev td{};
-        td.p = make_resamp_params(g.nsamples, g.n_unpadded, g.fft_size, g.dt, g.step_inv, t[off + k].P,
-                                  t[off + k].tau, t[off + k].Psi0);
-        td.n_steps = resamp_n_steps(td.p, kSinLut, kCosLut);
-        if (t[off + k].wu >= d.slots) return RADPUL_EVAL;
-        td.wu = t[off + k].wu;
-        td.mu0 = d.mu0s[td.wu];
-        d.h_tmpl.p[k] = td;
-        const float* th = thr + static_cast<size_t>(off + k) * thr_stride;
-        for (int h = 0; h < kNumHarmonicLevels; ++h) d.h_thr.p[k * hipk::kHsThrStride + h] = th[h];
-      }
-      hipGraphExec_t exec = nullptr;
-      auto it = d.graphs.find(nb);
-      static const bool use_graph = std::getenv("BRP_NO_GRAPH") == nullptr;
-      if (use_graph) {
-        if (it == d.graphs.end()) {
-          hipGraph_t graph;
-          BRP_HIP_CHECK(hipStreamBeginCapture(d.stream, hipStreamCaptureModeThreadLocal), RADPUL_HIP_GRAPH);
-          hipError_t e = d.enqueue(nb);
-          hipError_t e2 = hipStreamEndCapture(d.stream, &graph);
-          if (e != hipSuccess || e2 != hipSuccess) {
-            log_message(LOG_ERROR, true, "Graph capture failed: %s / %s\n", hipGetErrorName(e), hipGetErrorName(e2));
-            return RADPUL_HIP_GRAPH;
-          }
-          BRP_HIP_CHECK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0), RADPUL_HIP_GRAPH);
-          (void)hipGraphDestroy(graph);
-          d.graphs[nb] = exec;
-        } else {
-          exec = it->second;
-        }
-      }
-      if (d.fg_in) std::atomic_thread_fence(std::memory_order_seq_cst);  // BAR writes before the launch
-      BRP_HIP_CHECK(hipEventRecord(d.ev0, d.stream), RADPUL_HIP_KERNEL_INVOKE);
-      if (use_graph) {
-        BRP_HIP_CHECK(hipGraphLaunch(exec, d.stream), RADPUL_HIP_GRAPH);
-      } else {
-        BRP_HIP_CHECK(d.enqueue(nb), RADPUL_HIP_KERNEL_INVOKE);
-      }
-      BRP_HIP_CHECK(hipEventRecord(d.ev1, d.stream), RADPUL_HIP_KERNEL_INVOKE);
-    }
-    {
-      trace::Range wait("brp:batch_wait");
-      BRP_HIP_CHECK(hipStreamSynchronize(d.stream), RADPUL_HIP_KERNEL_INVOKE);
-    }
-    trace::Range decode("brp:batch_decode");
-    float ms = 0;
-    (void)hipEventElapsedTime(&ms, d.ev0, d.ev1);
-    d.st.gpu_ms += ms;
-    d.st.batches += 1;
-    if (d.shared_series != nullptr) d.st.shared_series_batches += 1;
-    d.st.templates += nb;
-    const uint32_t cnt = d.h_cands.p[0].x;
-    if (cnt > d.cap) {
-      log_message(LOG_ERROR, true, "Candidate overflow (%u > %u slots) in a batch of %d templates.\n", cnt, d.cap, nb);
-      return RADPUL_HIP_CAND_OVERFLOW;
-    }
-    const uint2* src = d.h_cands.p + 1;
-    std::vector<uint2> extra;
-    if (cnt > d.kcopy) {
-      extra.resize(cnt);
-      // stream-ordered (a null-stream copy would invalidate another engine's
-      // graph capture running in a sibling thread)
-      BRP_HIP_CHECK(hipMemcpyAsync(extra.data(), d.cands.p + 1, cnt * sizeof(uint2), hipMemcpyDeviceToHost, d.stream),
-                    RADPUL_HIP_MEM_COPY_DEVICE_HOST);
-      BRP_HIP_CHECK(hipStreamSynchronize(d.stream), RADPUL_HIP_MEM_COPY_DEVICE_HOST);
-      src = extra.data();
-      d.st.overflow_reruns += 1;
-    }
-    for (int k = 0; k < nb; ++k)
-      for (int h = 0; h < kNumHarmonicLevels; ++h) out[off + k].level[h].clear();
-    constexpr uint32_t kBinMask = (1u << hipk::kHsBinBits) - 1u;
-    for (uint32_t q = 0; q < cnt; ++q) {
-      const uint32_t key = src[q].x;
-      const uint32_t k = key >> 26, h = (key >> hipk::kHsBinBits) & 7u;
-      float p;
-      std::memcpy(&p, &src[q].y, sizeof(float));
-      out[off + k].level[h].push_back(BinPower{key & kBinMask, p});
-    }
-    for (int k = 0; k < nb; ++k)
-      for (int h = 0; h < kNumHarmonicLevels; ++h) {
-        std::vector<BinPower>& lv = out[off + k].level[h];
-        std::sort(lv.begin(), lv.end(), [](const BinPower& a, const BinPower& b) { return a.bin < b.bin; });
-      }
+  trace::Range launch("brp:batch_launch");
+  d.select_io(slot);
+  for (int k = 0; k < nb; ++k) {
+    TemplateDev td{};
+    td.p = make_resamp_params(g.nsamples, g.n_unpadded, g.fft_size, g.dt, g.step_inv, t[k].P, t[k].tau, t[k].Psi0);
+    td.n_steps = resamp_n_steps(td.p, kSinLut, kCosLut);
+    if (t[k].wu >= d.slots) return RADPUL_EVAL;
+    td.wu = t[k].wu;
+    td.mu0 = d.mu0s[td.wu];
+    d.h_tmpl.p[k] = td;
+    const float* th = thr + static_cast<size_t>(k) * thr_stride;
+    for (int h = 0; h < kNumHarmonicLevels; ++h) d.h_thr.p[k * hipk::kHsThrStride + h] = th[h];
   }
+  hipGraphExec_t exec = nullptr;
+  const int key = nb * Impl::kIoSlots + slot;
+  auto it = d.graphs.find(key);
+  static const bool use_graph = std::getenv("BRP_NO_GRAPH") == nullptr;
+  if (use_graph) {
+    if (it == d.graphs.end()) {
+      hipGraph_t graph;
+      BRP_HIP_CHECK(hipStreamBeginCapture(d.stream, hipStreamCaptureModeThreadLocal), RADPUL_HIP_GRAPH);
+      hipError_t e = d.enqueue(nb);
+      hipError_t e2 = hipStreamEndCapture(d.stream, &graph);
+      if (e != hipSuccess || e2 != hipSuccess) {
+        log_message(LOG_ERROR, true, "Graph capture failed: %s / %s\n", hipGetErrorName(e), hipGetErrorName(e2));
+        return RADPUL_HIP_GRAPH;
+      }
+      BRP_HIP_CHECK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0), RADPUL_HIP_GRAPH);
+      (void)hipGraphDestroy(graph);
+      d.graphs[key] = exec;
+    } else {
+      exec = it->second;
+    }
+  }
+  if (d.fg_in) std::atomic_thread_fence(std::memory_order_seq_cst);  // BAR writes before the launch
+  BRP_HIP_CHECK(hipEventRecord(d.ev0, d.stream), RADPUL_HIP_KERNEL_INVOKE);
+  if (use_graph) {
+    BRP_HIP_CHECK(hipGraphLaunch(exec, d.stream), RADPUL_HIP_GRAPH);
+  } else {
+    BRP_HIP_CHECK(d.enqueue(nb), RADPUL_HIP_KERNEL_INVOKE);
+  }
+  BRP_HIP_CHECK(hipEventRecord(d.ev1, d.stream), RADPUL_HIP_KERNEL_INVOKE);
+  d.io[slot].nb = nb;
+  d.io[slot].pending = true;
+  d.io_next = (slot + 1) % Impl::kIoSlots;
+  return 0;
+}
+
+int HipEngine::complete(std::vector<TemplateCands>& out) {
+  Impl& d = *impl_;
+  const int slot = d.io_head;
+  Impl::BatchIO& o = d.io[slot];
+  if (!o.pending) return RADPUL_EMISC;
+  BRP_HIP_CHECK(hipSetDevice(d.device), RADPUL_HIP_DEVICE_SET);
+  {
+    trace::Range wait("brp:batch_wait");
+    BRP_HIP_CHECK(hipEventSynchronize(o.ev1), RADPUL_HIP_KERNEL_INVOKE);
+  }
+  o.pending = false;
+  d.io_head = (slot + 1) % Impl::kIoSlots;
+  trace::Range decode("brp:batch_decode");
+  const int nb = o.nb;
+  float ms = 0;
+  (void)hipEventElapsedTime(&ms, o.ev0, o.ev1);
+  d.st.gpu_ms += ms;
+  d.st.batches += 1;
+  if (d.shared_series != nullptr) d.st.shared_series_batches += 1;
+  d.st.templates += nb;
+  const uint32_t cnt = o.h_cands_p[0].x;
+  if (cnt > d.cap) {
+    log_message(LOG_ERROR, true, "Candidate overflow (%u > %u slots) in a batch of %d templates.\n", cnt, d.cap, nb);
+    return RADPUL_HIP_CAND_OVERFLOW;
+  }
+  const uint2* src = o.h_cands_p + 1;
+  std::vector<uint2> extra;
+  if (cnt > d.kcopy) {
+    extra.resize(cnt);
+    // stream-ordered (a null-stream copy would invalidate another engine's
+    // graph capture running in a sibling thread); waits for a batch queued
+    // behind this one too, which writes only its own I/O slot
+    BRP_HIP_CHECK(hipMemcpyAsync(extra.data(), o.cands.p + 1, cnt * sizeof(uint2), hipMemcpyDeviceToHost, d.stream),
+                  RADPUL_HIP_MEM_COPY_DEVICE_HOST);
+    BRP_HIP_CHECK(hipStreamSynchronize(d.stream), RADPUL_HIP_MEM_COPY_DEVICE_HOST);
+    src = extra.data();
+    d.st.overflow_reruns += 1;
+  }
+  out.clear();
+  out.resize(nb);
+  constexpr uint32_t kBinMask = (1u << hipk::kHsBinBits) - 1u;
+  for (uint32_t q = 0; q < cnt; ++q) {
+    const uint32_t key = src[q].x;
+    const uint32_t k = key >> 26, h = (key >> hipk::kHsBinBits) & 7u;
+    float p;
+    std::memcpy(&p, &src[q].y, sizeof(float));
+    out[k].level[h].push_back(BinPower{key & kBinMask, p});
+  }
+  for (int k = 0; k < nb; ++k)
+    for (int h = 0; h < kNumHarmonicLevels; ++h) {
+      std::vector<BinPower>& lv = out[k].level[h];
+      std::sort(lv.begin(), lv.end(), [](const BinPower& a, const BinPower& b) { return a.bin < b.bin; });
+    }
   return 0;
 }
 
 int HipEngine::power_spectrum(const TemplateInput& t, std::vector<float>& ps_out, uint32_t* n_steps) {
   Impl& d = *impl_;
+  if (d.io_busy()) return RADPUL_EMISC;
+  d.select_io(0);
   const SearchGeometry& g = d.g;
   TemplateDev td{};
   td.p = make_resamp_params(g.nsamples, g.n_unpadded, g.fft_size, g.dt, g.step_inv, t.P, t.tau, t.Psi0);
@@ -1073,7 +1151,8 @@ int HipEngine::power_spectrum(const TemplateInput& t, std::vector<float>& ps_out
 
 int HipEngine::benchmark_stages(const TemplateInput* t, int n, int reps, std::vector<double>& us_per_launch) {
   Impl& d = *impl_;
-  if (!d.ready) return RADPUL_EMISC;
+  if (!d.ready || d.io_busy()) return RADPUL_EMISC;
+  d.select_io(0);
   const int nb = std::min(n, d.batch);
   const SearchGeometry& g = d.g;
   // BRP_STAGE_THR_SCALE: scale the chi^2 thresholds (harmonic-sum ablations:
@@ -1158,6 +1237,15 @@ class HipBackend final : public Backend {
               std::vector<TemplateCands>& out) override {
     return eng_.process(t, n, thr, out);
   }
+  // two batches in flight per pipeline (BRP_INFLIGHT=1: one, the previous behaviour)
+  int max_in_flight() const override {
+    static const int depth = std::getenv("BRP_INFLIGHT") ? std::max(1, std::atoi(std::getenv("BRP_INFLIGHT"))) : 2;
+    return std::min(depth, eng_.max_in_flight());
+  }
+  int submit(const TemplateInput* t, int n, const float thr[kNumHarmonicLevels]) override {
+    return eng_.submit(t, n, thr, 0);
+  }
+  int complete(std::vector<TemplateCands>& out) override { return eng_.complete(out); }
   // any HIP backend can take the first
   // backend's whitened series without a host round trip: pipelines on the same
   // device read it in place (adopt_series), other devices get a peer copy over

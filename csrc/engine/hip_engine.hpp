@@ -52,6 +52,14 @@ class HipEngine {
   int process(const TemplateInput* t, int n, const float thr[kNumHarmonicLevels], std::vector<TemplateCands>& out);
   // per-template thresholds thr[i * thr_stride + h] (thr_stride 0: shared)
   int process(const TemplateInput* t, int n, const float* thr, int thr_stride, std::vector<TemplateCands>& out);
+  // Pipelined form of process(): submit() launches one batch (n <= batch())
+  // and returns at once; complete() waits for the oldest submitted batch and
+  // decodes its candidates. Up to max_in_flight() batches may be submitted
+  // before the first complete(); process() and the test hooks need none
+  // outstanding.
+  int submit(const TemplateInput* t, int n, const float* thr, int thr_stride);
+  int complete(std::vector<TemplateCands>& out);
+  int max_in_flight() const;
   // test hooks
   int power_spectrum(const TemplateInput& t, std::vector<float>& ps, uint32_t* n_steps);
   // time each pipeline stage (prologue, pass1, pass2, pass3, harmonic, epilogue,
