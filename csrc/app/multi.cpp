@@ -6,6 +6,7 @@
 #include <condition_variable>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <map>
 #include <mutex>
 #include <thread>
@@ -228,33 +229,53 @@ int MultiSession::run(const std::vector<uint32_t>& begins, uint32_t end, std::ve
     ti.wu = w;
     return ti;
   };
+  // up to max_in_flight() batches submitted per engine (the next launched while
+  // the previous runs), completed in submission order
   auto worker = [&](HipEngine* eng) {
+    const int depth = std::max(1, eng->max_in_flight());
+    std::deque<Batch> inflight;
     std::vector<float> thr;
-    for (;;) {
-      boinc::suspend_point();  // no GPU work starts while the client has the task suspended
-      if (stop.load()) return;
-      const uint64_t first = next.fetch_add(static_cast<uint64_t>(B));
-      if (first >= npairs) return;
-      const int n = static_cast<int>(std::min<uint64_t>(B, npairs - first));
-      Batch bt;
-      bt.first = first;
-      thr.assign(static_cast<size_t>(n) * kNumHarmonicLevels, 0.0f);
-      for (int i = 0; i < n; ++i) bt.tin.push_back(pair_input(first + i));
+    auto publish = [&](Batch&& bt) {
       {
         std::lock_guard<std::mutex> lk(mu);
-        for (int i = 0; i < n; ++i)
-          std::memcpy(&thr[static_cast<size_t>(i) * kNumHarmonicLevels],
-                      &thr_wu[static_cast<size_t>(bt.tin[i].wu) * kNumHarmonicLevels],
-                      sizeof(float) * kNumHarmonicLevels);
-      }
-      boinc::begin_critical_section();
-      bt.rc = eng->process(bt.tin.data(), n, thr.data(), kNumHarmonicLevels, bt.cands);
-      boinc::end_critical_section();
-      {
-        std::lock_guard<std::mutex> lk(mu);
-        ready.emplace(first, std::move(bt));
+        const uint64_t f = bt.first;
+        ready.emplace(f, std::move(bt));
       }
       cv.notify_all();
+    };
+    for (;;) {
+      while (static_cast<int>(inflight.size()) < depth) {
+        boinc::suspend_point();  // no GPU work starts while the client has the task suspended
+        if (stop.load()) break;
+        const uint64_t first = next.fetch_add(static_cast<uint64_t>(B));
+        if (first >= npairs) break;
+        const int n = static_cast<int>(std::min<uint64_t>(B, npairs - first));
+        Batch bt;
+        bt.first = first;
+        thr.assign(static_cast<size_t>(n) * kNumHarmonicLevels, 0.0f);
+        for (int i = 0; i < n; ++i) bt.tin.push_back(pair_input(first + i));
+        {
+          std::lock_guard<std::mutex> lk(mu);
+          for (int i = 0; i < n; ++i)
+            std::memcpy(&thr[static_cast<size_t>(i) * kNumHarmonicLevels],
+                        &thr_wu[static_cast<size_t>(bt.tin[i].wu) * kNumHarmonicLevels],
+                        sizeof(float) * kNumHarmonicLevels);
+        }
+        boinc::begin_critical_section();
+        bt.rc = eng->submit(bt.tin.data(), n, thr.data(), kNumHarmonicLevels);  // copies its inputs
+        if (bt.rc) {
+          boinc::end_critical_section();
+          publish(std::move(bt));
+          continue;
+        }
+        inflight.push_back(std::move(bt));
+      }
+      if (inflight.empty()) return;
+      Batch bt = std::move(inflight.front());
+      inflight.pop_front();
+      bt.rc = eng->complete(bt.cands);
+      boinc::end_critical_section();
+      publish(std::move(bt));
     }
   };
   std::vector<std::thread> threads;

@@ -966,7 +966,11 @@ int HipEngine::process(const TemplateInput* t, int n, const float* thr, int thr_
   return 0;
 }
 
-int HipEngine::max_in_flight() const { return Impl::kIoSlots; }
+// two batches in flight per pipeline (BRP_INFLIGHT=1: one, the previous behaviour)
+int HipEngine::max_in_flight() const {
+  static const int depth = std::getenv("BRP_INFLIGHT") ? std::max(1, std::atoi(std::getenv("BRP_INFLIGHT"))) : 2;
+  return std::min(depth, Impl::kIoSlots);
+}
 
 int HipEngine::submit(const TemplateInput* t, int nb, const float* thr, int thr_stride) {
   Impl& d = *impl_;
@@ -1237,11 +1241,7 @@ class HipBackend final : public Backend {
               std::vector<TemplateCands>& out) override {
     return eng_.process(t, n, thr, out);
   }
-  // two batches in flight per pipeline (BRP_INFLIGHT=1: one, the previous behaviour)
-  int max_in_flight() const override {
-    static const int depth = std::getenv("BRP_INFLIGHT") ? std::max(1, std::atoi(std::getenv("BRP_INFLIGHT"))) : 2;
-    return std::min(depth, eng_.max_in_flight());
-  }
+  int max_in_flight() const override { return eng_.max_in_flight(); }
   int submit(const TemplateInput* t, int n, const float thr[kNumHarmonicLevels]) override {
     return eng_.submit(t, n, thr, 0);
   }
