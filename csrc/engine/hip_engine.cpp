@@ -999,7 +999,10 @@ int HipEngine::submit(const TemplateInput* t, int nb, const float* thr, int thr_
   hipGraphExec_t exec = nullptr;
   const int key = nb * Impl::kIoSlots + slot;
   auto it = d.graphs.find(key);
-  static const bool use_graph = std::getenv("BRP_NO_GRAPH") == nullptr;
+  // Direct launches into the stream by default: with two batches in flight the
+  // launch cost is hidden, and replaying the batch as a HIP graph measured
+  // 2-4 % slower (profiles/README.md). BRP_GRAPH=1 replays captured graphs.
+  static const bool use_graph = std::getenv("BRP_GRAPH") != nullptr && std::atoi(std::getenv("BRP_GRAPH")) != 0;
   if (use_graph) {
     if (it == d.graphs.end()) {
       hipGraph_t graph;
