@@ -264,7 +264,7 @@ struct HipEngine::Impl {
     int nb = 0;
     bool pending = false;
   };
-  static constexpr int kIoSlots = 2;
+  static constexpr int kIoSlots = 3;  // I/O slots; BRP_INFLIGHT picks how many are used (default 2)
   BatchIO io[kIoSlots];
   int io_cur = 0, io_next = 0, io_head = 0;
   // views of slot io_cur, used by enqueue_stage / capture and the test hooks
@@ -286,7 +286,11 @@ struct HipEngine::Impl {
     ev0 = o.ev0;
     ev1 = o.ev1;
   }
-  bool io_busy() const { return io[0].pending || io[1].pending; }
+  bool io_busy() const {
+    for (const BatchIO& o : io)
+      if (o.pending) return true;
+    return false;
+  }
   DevBuf<float2> tw_hi, tw_lo;
   DevBuf<float2> w_spec, w_z;   // whitening scratch: half spectrum, packed inverse input
   DevBuf<float> w_psw, w_med;   // whitening scratch: power spectrum, running median
@@ -966,7 +970,7 @@ int HipEngine::process(const TemplateInput* t, int n, const float* thr, int thr_
   return 0;
 }
 
-// two batches in flight per pipeline (BRP_INFLIGHT=1: one, the previous behaviour)
+// two batches in flight per pipeline (BRP_INFLIGHT=1: one, the previous behaviour; 3: three)
 int HipEngine::max_in_flight() const {
   static const int depth = std::getenv("BRP_INFLIGHT") ? std::max(1, std::atoi(std::getenv("BRP_INFLIGHT"))) : 2;
   return std::min(depth, Impl::kIoSlots);
