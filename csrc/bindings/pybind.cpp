@@ -448,6 +448,21 @@ PYBIND11_MODULE(_brp, m) {
              return cands_to_list(out);
            })
       .def("set_ps_fp16", [](HipEngine& e, bool on) { e.set_ps_fp16(on); })
+      .def("submit",
+           [](HipEngine& e, py::array_t<float> P, py::array_t<float> tau, py::array_t<float> psi, std::vector<float> thr) {
+             auto t = arrays_to_templates(P, tau, psi);
+             check(e.submit(t.data(), static_cast<int>(t.size()), thr.data(), 0), "HipEngine.submit");
+           })
+      .def("complete",
+           [](HipEngine& e) {
+             std::vector<TemplateCands> out;
+             {
+               py::gil_scoped_release rel;
+               check(e.complete(out), "HipEngine.complete");
+             }
+             return cands_to_list(out);
+           })
+      .def("max_in_flight", &HipEngine::max_in_flight)
       .def("adopt_series", [](HipEngine& e, const HipEngine& src) { check(e.adopt_series(src), "HipEngine.adopt_series"); })
       .def("power_spectrum",
            [](HipEngine& e, float P, float tau, float psi) {

@@ -143,6 +143,37 @@ def test_harmonic_sum_fp16_pruned_equals_full(brp, gpu, monkeypatch, thr):
             np.testing.assert_array_equal(outs["0"][k][h][1], outs["1"][k][h][1])
 
 
+def test_engine_batches_in_flight_match_process(brp, gpu):
+    """Pipelined engine API: max_in_flight() batches submitted back to back
+    (double-buffered parameters and candidate lists, one stream) complete in
+    submission order with the candidates process() gives one batch at a time;
+    process() refuses to run while batches are outstanding."""
+    hdr, series, _ = brp.read_work_unit(str(WU))
+    opt = dict(OPT_BENCH, white=True)
+    geom = brp.derive_geometry(hdr, opt)
+    eng = _engine(brp, geom, series, batch=1)
+    eng.whiten(opt, brp.read_zaplist(str(ZAP)), series)
+    P, tau, psi = (x.astype(np.float32) for x in brp.read_template_bank(str(BANK)))
+    thr = [9.0, 12.0, 16.0, 22.0, 33.0]
+    depth = eng.max_in_flight()
+    assert depth >= 2
+    ref = [eng.process(P[k:k + 1], tau[k:k + 1], psi[k:k + 1], thr)[0] for k in range(depth + 1)]
+    for k in range(depth):
+        eng.submit(P[k:k + 1], tau[k:k + 1], psi[k:k + 1], thr)
+    with pytest.raises(Exception):
+        eng.process(P[:1], tau[:1], psi[:1], thr)
+    got = [eng.complete()[0]]
+    eng.submit(P[depth:depth + 1], tau[depth:depth + 1], psi[depth:depth + 1], thr)  # reuses a completed slot
+    got += [eng.complete()[0] for _ in range(depth)]
+    assert sum(len(ref[k][h][0]) for k in range(depth + 1) for h in range(5)) > 0
+    for k in range(depth + 1):
+        for h in range(5):
+            np.testing.assert_array_equal(got[k][h][0], ref[k][h][0])
+            np.testing.assert_array_equal(got[k][h][1], ref[k][h][1])
+    with pytest.raises(Exception):
+        eng.complete()  # nothing outstanding
+
+
 def test_whitening_wide_window_matches_cpu(brp, gpu, tmp_path):
     """-B above the LDS kernel's 3072: whitening stays on the device (wide
     running median) and matches the CPU whitening."""
