@@ -58,13 +58,15 @@ class SearchOutput:
 class BRPSearch:
     """Search one work unit with the native driver (C++ host loop, HIP kernels)."""
 
-    def __init__(self, config: SearchConfig, gpus: int = 1):
+    def __init__(self, config: SearchConfig, gpus: int = 1, pipelines: int = 1):
         self.config = config
-        self.gpus = gpus
+        self.gpus = gpus            # devices (CPU backend: worker threads)
+        self.pipelines = pipelines  # HIP pipelines (stream + buffers + host thread) per device
         self.brp = native()
 
     def run(self, begin: int = 0, end: int = 0, write_output: bool = True, use_checkpoint: bool = True) -> SearchOutput:
-        r = self.brp.run_search(self.config.options(), begin, end, write_output, use_checkpoint, self.gpus)
+        r = self.brp.run_search(self.config.options(), begin, end, write_output, use_checkpoint, self.gpus,
+                                self.pipelines)
         return SearchOutput(table=r["table"], geometry=r["geometry"], templates_total=r["templates_total"],
                             templates_run=r["templates_run"], interrupted=r["interrupted"],
                             timings=dict(setup=r["t_setup"], templates=r["t_templates"], total=r["t_total"],

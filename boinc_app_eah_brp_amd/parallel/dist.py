@@ -183,6 +183,27 @@ def merge_tables(tables) -> object:
     return out
 
 
+def table_floors(table) -> list[float]:
+    """Per harmonic level the power of the 100th entry (0 while the level is
+    not full): what a new candidate must beat (demod_binary.c:1281)."""
+    ent = table.entries()
+    return [float(ent[h * 100 + 99][1]) if ent[h * 100 + 99][5] > 0 else 0.0 for h in range(5)]
+
+
+def max_floors_over_ranks(floors: list[float], ctx: DistContext) -> list[float]:
+    """Element-wise max of the five level floors over the ranks (one 40-byte
+    all-reduce): a valid global floor, since every rank's 100 entries of a
+    level are distinct bins the merged table also holds at >= that power."""
+    if not ctx.distributed:
+        return list(floors)
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor(floors, dtype=torch.float64, device=ctx.device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [float(v) for v in t.cpu().tolist()]
+
+
 def barrier(ctx: DistContext) -> None:
     if ctx.distributed:
         import torch.distributed as dist
@@ -270,13 +291,24 @@ class ShardedSearch:
         self.session.prepare()
         t1 = time.perf_counter()
         search_s = 0.0
+        self.seed_floors = []  # per chunk: the level floors every rank started from (tests)
         while n < self.total:
             hi = min(self.total, n + max(1, chunk))
+            # Global pruning: every rank starts its part of the chunk from the
+            # merged table of the prefix, identical on all ranks after the
+            # all-gather, so its device and host thresholds are the global
+            # 100th-place floors (demod_binary.c:1268-1282 semantics), not those
+            # of its own emptier table. Re-merging the seeded entries is exact:
+            # the merge keeps one entry per bin and the same entry wins.
+            seed = table.to_bytes()
+            self.seed_floors.append(table_floors(table))
 
-            def run_shard(begin, end, lo=n):
+            def run_shard(begin, end, lo=n, seed=seed):
                 nonlocal search_s
                 ts = time.perf_counter()
-                t, _ = self.session.run(lo + begin, lo + end, brp.CandidateTable())
+                start = brp.CandidateTable()
+                start.from_bytes(np.asarray(seed, dtype=np.uint8).copy())
+                t, _ = self.session.run(lo + begin, lo + end, start)
                 search_s += time.perf_counter() - ts
                 return [t]
 

@@ -48,6 +48,8 @@ void print_usage(const char* prog) {
   std::printf(" --mi355x-no-checkpoint\t\tboolean\tNever read or write checkpoints (Debian NOCHECKPOINTING build).\n");
   std::printf(" --mi355x-progress-every\tinteger\tReport fraction done every N templates (Debian COMMUNICATIONREDUCTION).\n");
   std::printf(" --mi355x-sequential-passes\tboolean\tRun several -i/-o pairs one after another instead of batched.\n");
+  std::printf(" --mi355x-dump-dir\t\tstring\tWith -z: write the whitened series and template 0's resampled series and\n"
+              "\t\t\t\t\tpower spectrum as text (one value per line) into this directory.\n");
   std::printf("\n");
 }
 
@@ -201,6 +203,10 @@ int parse_search_args(int argc, char** argv, SearchOptions& opt, SearchControl& 
     } else if (std::strcmp(a, "--mi355x-cpu") == 0) {
       opt.use_cpu = true;
       i++;
+    } else if (std::strcmp(a, "--mi355x-dump-dir") == 0) {
+      if (!v) return RADPUL_EFILE;
+      opt.dump_dir = v;
+      i += 2;
     } else if (is(a, "-h", "--help")) {
       print_usage(argv[0]);
       return RADPUL_EMISC;
@@ -267,6 +273,7 @@ int wrapper_main(int argc, char** argv) {
                                          {"mi355x-no-checkpoint", no_argument, 0, 1007},
                                          {"mi355x-progress-every", required_argument, 0, 1008},
                                          {"mi355x-sequential-passes", no_argument, 0, 1009},
+                                         {"mi355x-dump-dir", required_argument, 0, 1010},
                                          {0, 0, 0, 0}};
   optind = 1;
   auto file_arg = [&](const char* opt, const char* val) {
@@ -311,6 +318,7 @@ int wrapper_main(int argc, char** argv) {
       case 1007: fwd.push_back("--mi355x-no-checkpoint"); break;
       case 1008: fwd.push_back("--mi355x-progress-every"); fwd.push_back(optarg); break;
       case 1009: sequential = true; break;
+      case 1010: fwd.push_back("--mi355x-dump-dir"); fwd.push_back(optarg); break;
       default: boinc::finish(EINSTEINRADIO_EOPT);
     }
   }

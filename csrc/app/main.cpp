@@ -6,6 +6,7 @@
 #include "../boinc/runtime.hpp"
 #include "../core/errors.hpp"
 #include "../core/log.hpp"
+#include "../core/trace.hpp"
 #include "search.hpp"
 
 int main(int argc, char** argv) {
@@ -14,6 +15,7 @@ int main(int argc, char** argv) {
   brp::crash::install();
   brp::log_message(brp::LOG_DEBUG, true, "Initializing BOINC...\n");
   brp::boinc::init(argc, argv);
+  brp::trace::phase("boinc runtime init");
   brp::log_message(brp::LOG_DEBUG, true, "Calling worker, let's get started...\n");
   const int result = brp::wrapper_main(argc, argv);
   if (brp::is_transient_resource_error(result)) {
@@ -22,6 +24,7 @@ int main(int argc, char** argv) {
     brp::log_message(brp::LOG_WARN, false, "Returning control to BOINC, delaying next attempt for at least 15 minutes...\n");
     brp::boinc::temporary_exit(900, "Not enough free CPU/GPU memory available! Delaying next attempt for at least 15 minutes...");
   }
+  brp::trace::phase("worker returned");
   brp::log_message(brp::LOG_DEBUG, true, "Shutting down BOINC... Bye!\n");
   brp::boinc::finish(result);
 }

@@ -221,6 +221,20 @@ int MultiSession::run(const std::vector<uint32_t>& begins, uint32_t end, std::ve
   }
   const uint64_t npairs = order.size();
   if (npairs == 0) return 0;
+  // batches never cross a deal block: when the WUs resume from different
+  // templates a block is not a multiple of B pairs, and a batch spanning two
+  // blocks would put templates past the block's checkpoint prefix into the
+  // tables that checkpoint describes
+  std::vector<uint64_t> bstart;
+  {
+    uint64_t q = 0;
+    for (const auto& blk : blocks) {
+      for (; q < blk.first; q += static_cast<uint64_t>(B)) bstart.push_back(q);
+      q = blk.first;
+    }
+    bstart.push_back(npairs);
+  }
+  const uint64_t nbatches = bstart.size() - 1;
   auto pair_input = [&](uint64_t q) {
     const uint32_t t = order[q].first;
     const uint32_t w = order[q].second;
@@ -247,9 +261,10 @@ int MultiSession::run(const std::vector<uint32_t>& begins, uint32_t end, std::ve
       while (static_cast<int>(inflight.size()) < depth) {
         boinc::suspend_point();  // no GPU work starts while the client has the task suspended
         if (stop.load()) break;
-        const uint64_t first = next.fetch_add(static_cast<uint64_t>(B));
-        if (first >= npairs) break;
-        const int n = static_cast<int>(std::min<uint64_t>(B, npairs - first));
+        const uint64_t bi = next.fetch_add(1);
+        if (bi >= nbatches) break;
+        const uint64_t first = bstart[bi];
+        const int n = static_cast<int>(bstart[bi + 1] - first);
         Batch bt;
         bt.first = first;
         thr.assign(static_cast<size_t>(n) * kNumHarmonicLevels, 0.0f);

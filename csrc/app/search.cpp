@@ -23,6 +23,7 @@
 #include "../core/io.hpp"
 #include "../core/log.hpp"
 #include "../core/stats.hpp"
+#include "../core/cpu_backend.hpp"
 
 #ifndef BRP_GIT_ID
 #define BRP_GIT_ID "unknown"
@@ -178,8 +179,10 @@ int SearchSession::open(const SearchOptions& opt, const SearchControl& ctl) {
   Impl& d = *impl_;
   d.opt = opt;
   d.ctl = ctl;
+  trace::phase("open");
   int rc = read_template_bank(opt.templatebank, d.bank);
   if (rc) return rc;
+  trace::phase("bank read");
   log_message(LOG_DEBUG, true, "Total amount of templates: %zu\n", d.bank.size());
   d.tin.resize(d.bank.size());
   for (size_t t = 0; t < d.bank.size(); ++t)
@@ -187,6 +190,7 @@ int SearchSession::open(const SearchOptions& opt, const SearchControl& ctl) {
                              static_cast<float>(d.bank.Psi0[t])};
   rc = read_work_unit(opt.inputfile, d.wu);
   if (rc) return rc;
+  trace::phase("work unit read");
   if (opt.debug) log_header(d.wu.header);
   sky_position(d.wu.header, d.info);
   rc = derive_geometry(d.wu.header, opt, d.g);
@@ -249,6 +253,7 @@ int SearchSession::open(const SearchOptions& opt, const SearchControl& ctl) {
     d.backends.push_back(std::move(b));
   }
   boinc::end_critical_section();
+  trace::phase("backends created");
   return 0;
 }
 
@@ -285,11 +290,17 @@ int SearchSession::prepare() {
     boinc::end_critical_section();
     return rc;
   }
+  trace::phase("pipeline 0 set up + whitened");
   SearchOptions opt_nw = d.opt;
   opt_nw.white = false;
   opt_nw.prewhitened = d.opt.white;
   for (size_t k = 1; k < nb; ++k) {
-    if (d.backends[k]->setup_from(*d.backends[src[k]], d.g) == 0) continue;
+    rc = d.backends[k]->setup_from(*d.backends[src[k]], d.g);
+    if (rc == 0) continue;
+    if (rc > 0) {  // e.g. RADPUL_HIP_MEM_ALLOC_DEVICE: the wrapper's temporary exit
+      boinc::end_critical_section();
+      return rc;
+    }
     if (device_all) {
       // the host never received the whitened series
       log_message(LOG_ERROR, true, "Pipeline %zu could not take the whitened series from pipeline %zu.\n", k, src[k]);
@@ -304,7 +315,35 @@ int SearchSession::prepare() {
     }
   }
   boinc::end_critical_section();
+  trace::phase("pipelines set up");
+  if (d.opt.debug && !d.opt.dump_dir.empty() && !d.tin.empty()) return dump_debug_buffers();
   return 0;
+}
+
+// -z with a dump directory: the searched (whitened) series, template 0's
+// resampled series and its power spectrum as text, one value per line
+// (reference dumpFloatBufferToTextFile, erp_utilities.cpp:216-233, and the
+// device-buffer variant cuda_utilities.c:283-320). The resampled series comes
+// from the host model: the device gather uses the same nearest indices bit for
+// bit but never materialises the series (it is fused into FFT pass 1).
+int SearchSession::dump_debug_buffers() {
+  Impl& d = *impl_;
+  std::vector<float> series, ps, x;
+  boinc::begin_critical_section();
+  int rc = d.backends[0]->debug_buffers(d.tin[0], series, ps);
+  boinc::end_critical_section();
+  if (rc) {
+    log_message(LOG_WARN, true, "Debug buffers not available from the %s backend.\n", d.backends[0]->name());
+    return 0;
+  }
+  const TemplateInput& t = d.tin[0];
+  const ResampParams p = make_resamp_params(d.g.nsamples, d.g.n_unpadded, d.g.fft_size, d.g.dt, d.g.step_inv, t.P,
+                                            t.tau, t.Psi0);
+  cpu_resample(series.data(), p, x, nullptr, nullptr);
+  const std::string dir = d.opt.dump_dir + "/";
+  if ((rc = dump_float_buffer(series.data(), series.size(), dir + "dump_series.txt"))) return rc;
+  if ((rc = dump_float_buffer(x.data(), x.size(), dir + "dump_resampled_t0.txt"))) return rc;
+  return dump_float_buffer(ps.data(), ps.size(), dir + "dump_power_t0.txt");
 }
 
 int SearchSession::run(uint32_t begin, uint32_t end, CandidateTable& table, SearchResult& res,
@@ -552,6 +591,7 @@ int run_search(const SearchOptions& opt, const SearchControl& ctl, SearchResult&
   };
   rc = session.run(begin, end, table, res, hook);
   res.t_templates = now_s() - t_loop;
+  trace::phase("templates done");
   res.templates_done = counter;
   res.stats = session.stats();
   if (rc) return rc;
@@ -567,6 +607,7 @@ int run_search(const SearchOptions& opt, const SearchControl& ctl, SearchResult&
     trace::Range range("brp:finalize_output");
     rc = finalize_output(opt, g, counter, table, "einsteinbinary_mi355x");
     if (rc) return rc;
+    trace::phase("output written");
   }
   log_message(LOG_INFO, true,
               "Statistics: count dirty SumSpec pages %llu (not checkpointed), Page Size %d, fundamental_idx_hi-window_2: %u\n",

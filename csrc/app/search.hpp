@@ -51,6 +51,8 @@ class SearchSession {
   int open(const SearchOptions& opt, const SearchControl& ctl);
   // (re)upload the raw series and whiten it on the device(s); required before run()
   int prepare();
+  // -z + dump directory: write the debug buffer dumps (called by prepare())
+  int dump_debug_buffers();
   // process templates [begin, end) and apply them in template order to `table`
   int run(uint32_t begin, uint32_t end, CandidateTable& table, SearchResult& res, const TemplateHook& hook);
   const SearchGeometry& geometry() const;

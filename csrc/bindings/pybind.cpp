@@ -114,6 +114,7 @@ SearchOptions dict_to_options(const py::dict& d) {
   if (d.contains("templatebank")) o.templatebank = d["templatebank"].cast<std::string>();
   if (d.contains("checkpointfile")) o.checkpointfile = d["checkpointfile"].cast<std::string>();
   if (d.contains("zaplistfile")) o.zaplistfile = d["zaplistfile"].cast<std::string>();
+  if (d.contains("dump_dir")) o.dump_dir = d["dump_dir"].cast<std::string>();
   return o;
 }
 
@@ -439,6 +440,8 @@ PYBIND11_MODULE(_brp, m) {
            })
       .def("process",
            [](HipEngine& e, py::array_t<float> P, py::array_t<float> tau, py::array_t<float> psi, std::vector<float> thr) {
+             if (thr.size() < static_cast<size_t>(kNumHarmonicLevels))
+               throw py::value_error("HipEngine.process: need one threshold per harmonic level (5)");
              auto t = arrays_to_templates(P, tau, psi);
              std::vector<TemplateCands> out;
              {
@@ -450,6 +453,8 @@ PYBIND11_MODULE(_brp, m) {
       .def("set_ps_fp16", [](HipEngine& e, bool on) { e.set_ps_fp16(on); })
       .def("submit",
            [](HipEngine& e, py::array_t<float> P, py::array_t<float> tau, py::array_t<float> psi, std::vector<float> thr) {
+             if (thr.size() < static_cast<size_t>(kNumHarmonicLevels))
+               throw py::value_error("HipEngine.submit: need one threshold per harmonic level (5)");
              auto t = arrays_to_templates(P, tau, psi);
              check(e.submit(t.data(), static_cast<int>(t.size()), thr.data(), 0), "HipEngine.submit");
            })
@@ -505,6 +510,11 @@ PYBIND11_MODULE(_brp, m) {
     FFTPlan3 p;
     if (!make_fft_plan(M, p)) return py::none();
     return py::make_tuple(p.L1, p.L2, p.L3);
+  });
+  m.def("bluestein_plan", [](uint32_t Mb) -> py::object {
+    FFTPlan3 p;
+    if (!make_bluestein_plan(Mb, p)) return py::none();
+    return py::make_tuple(p.M, p.L1, p.L2, p.L3);
   });
 
   // ---------------------------------------------------------------- driver

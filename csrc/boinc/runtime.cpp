@@ -18,6 +18,7 @@
 #include <thread>
 
 #include "../core/log.hpp"
+#include "../core/trace.hpp"
 #include "client_shm.hpp"
 
 namespace brp {
@@ -340,8 +341,13 @@ double dtime() {
   return duration<double>(system_clock::now().time_since_epoch()).count();
 }
 
+// libboinc names the graphics segment after the slot the client runs the task
+// in ("boinc_<app>_<slot>", graphics2_util.cpp), so two tasks on one host do
+// not share it; standalone runs (no init_data.xml slot) use slot 0, which the
+// reference's runall.sh polls (debian/extra/einstein_bench/runall.sh)
 char* graphics_make_shmem(const char* app_name, int size) {
-  const std::string path = std::string("boinc_") + app_name + "_0";
+  const int slot = g_init.slot >= 0 ? g_init.slot : 0;
+  const std::string path = std::string("boinc_") + app_name + "_" + std::to_string(slot);
   const int fd = ::open(path.c_str(), O_RDWR | O_CREAT, 0666);
   if (fd < 0) return nullptr;
   if (ftruncate(fd, size) != 0) {
@@ -365,6 +371,7 @@ void finish(int status) {
   char text[32];
   std::snprintf(text, sizeof(text), "%d\n", status);
   write_marker(kFinishCalledFile, text);
+  trace::phase("finish");
   std::fflush(nullptr);
   if (g_lock_fd >= 0) ::close(g_lock_fd);
   std::exit(status);

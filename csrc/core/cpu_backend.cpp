@@ -141,6 +141,10 @@ int cpu_whiten(std::vector<float>& series, const SearchGeometry& g, const Search
   for (uint32_t i = 0; i < g.n_unpadded; ++i) x[i] = series[i];
   std::vector<cd> X;
   rfft_forward(x, X);
+  // odd N: fft_size = (N+1)/2 + 1 reaches one bin past the r2c output (the
+  // reference reads an unwritten FFTW slot there); use the DFT's own value,
+  // X_{(N+1)/2} = conj(X_{(N-1)/2})
+  while (X.size() < fft_size) X.push_back(std::conj(X[n - X.size()]));
   // fft in single precision like the reference buffers
   std::vector<float> re(fft_size), im(fft_size);
   for (uint32_t k = 0; k < fft_size; ++k) {

@@ -29,9 +29,40 @@ cd twiddle(size_t j, size_t n) {
 CpuFFT::CpuFFT(size_t n) : n_(n) {
   if (n == 0) throw std::invalid_argument("FFT size 0");
   factors_ = factorize(n);
+  if (factors_.back() > kMaxDirectPrime) {
+    // chirp w_j = exp(-pi i j^2 / n) with j^2 reduced mod 2n exactly
+    size_t L = 1;
+    while (L < 2 * n - 1) L <<= 1;
+    chirp_.resize(n);
+    for (size_t j = 0; j < n; ++j) {
+      const unsigned __int128 jj = static_cast<unsigned __int128>(j) * j;
+      chirp_[j] = twiddle(static_cast<size_t>(jj % (2 * n)), 2 * n);
+    }
+    conv_ = std::make_unique<CpuFFT>(L);
+    hspec_.assign(L, cd(0, 0));
+    hspec_[0] = std::conj(chirp_[0]);
+    for (size_t j = 1; j < n; ++j) hspec_[j] = hspec_[L - j] = std::conj(chirp_[j]);
+    conv_->forward(hspec_.data());
+    return;
+  }
   tw_.resize(n);
   for (size_t j = 0; j < n; ++j) tw_[j] = twiddle(j, n);
   scratch_.resize(n);
+}
+
+CpuFFT::~CpuFFT() = default;
+
+// X_k = w_k sum_j (x_j w_j) conj(w_{k-j}): one forward and one inverse FFT of
+// length L plus the precomputed spectrum of the conjugate chirp
+void CpuFFT::bluestein(cd* data) {
+  const size_t L = conv_->size();
+  std::vector<cd> y(L, cd(0, 0));
+  for (size_t j = 0; j < n_; ++j) y[j] = data[j] * chirp_[j];
+  conv_->forward(y.data());
+  for (size_t k = 0; k < L; ++k) y[k] *= hspec_[k];
+  conv_->inverse(y.data());
+  const double inv_l = 1.0 / static_cast<double>(L);
+  for (size_t k = 0; k < n_; ++k) data[k] = y[k] * chirp_[k] * inv_l;
 }
 
 void CpuFFT::rec(const cd* in, size_t istride, cd* out, size_t n, size_t fac_idx, size_t tw_stride, bool inv) {
@@ -81,11 +112,18 @@ void CpuFFT::rec(const cd* in, size_t istride, cd* out, size_t n, size_t fac_idx
 }
 
 void CpuFFT::forward(cd* data) {
+  if (conv_) return bluestein(data);
   rec(data, 1, scratch_.data(), n_, 0, 1, false);
   std::copy(scratch_.begin(), scratch_.end(), data);
 }
 
 void CpuFFT::inverse(cd* data) {
+  if (conv_) {  // conj(DFT(conj x))
+    for (size_t j = 0; j < n_; ++j) data[j] = std::conj(data[j]);
+    bluestein(data);
+    for (size_t j = 0; j < n_; ++j) data[j] = std::conj(data[j]);
+    return;
+  }
   rec(data, 1, scratch_.data(), n_, 0, 1, true);
   std::copy(scratch_.begin(), scratch_.end(), data);
 }
@@ -122,7 +160,8 @@ void rfft_inverse(const std::vector<cd>& Xin, size_t n, std::vector<double>& x) 
   if (n % 2 == 0) X[n / 2] = cd(X[n / 2].real(), 0);
   if (n % 2) {
     std::vector<cd> z(n);
-    for (size_t k = 0; k < n; ++k) z[k] = (k < X.size()) ? X[k] : std::conj(X[n - k]);
+    // c2r of odd length reads bins 0 .. (n-1)/2 only (FFTW semantics)
+    for (size_t k = 0; k < n; ++k) z[k] = (k <= n / 2) ? X[k] : std::conj(X[n - k]);
     CpuFFT(n).inverse(z.data());
     for (size_t i = 0; i < n; ++i) x[i] = z[i].real();
     return;

@@ -7,6 +7,7 @@
 
 #include <complex>
 #include <cstddef>
+#include <memory>
 #include <vector>
 
 namespace brp {
@@ -16,6 +17,7 @@ using cd = std::complex<double>;
 class CpuFFT {
  public:
   explicit CpuFFT(size_t n);
+  ~CpuFFT();
   size_t size() const { return n_; }
   // In-place complex DFT, forward = exp(-2 pi i nk/N), unnormalised.
   void forward(cd* data);
@@ -23,10 +25,18 @@ class CpuFFT {
 
  private:
   void rec(const cd* in, size_t istride, cd* out, size_t n, size_t fac_idx, size_t tw_stride, bool inv);
+  void bluestein(cd* data);
   size_t n_;
   std::vector<size_t> factors_;
   std::vector<cd> tw_;  // exp(-2 pi i j / n)
   std::vector<cd> scratch_;
+  // Lengths with a prime factor above kMaxDirectPrime (any padding -P of the
+  // reference gives such N) run as a chirp-z convolution (Bluestein) over a
+  // power-of-two FFT of length >= 2n - 1, in double precision.
+  static constexpr size_t kMaxDirectPrime = 64;
+  std::unique_ptr<CpuFFT> conv_;  // length-L transform of the convolution
+  std::vector<cd> chirp_;    // exp(-pi i j^2 / n), j < n
+  std::vector<cd> hspec_;    // FFT_L of the conjugate chirp, wrapped
 };
 
 // Real -> half-complex (fft_size = N/2+1 outputs), unnormalised (FFTW r2c semantics).

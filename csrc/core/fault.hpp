@@ -6,7 +6,8 @@
 //   BRP_FAULT=<fault>[,<fault>...]     fault = name | name:param
 //
 //   kill_after_template:N  request a BOINC quit once N templates are done
-//   hip_oom                every device allocation fails (-> temporary exit)
+//   hip_oom[:N]            every device allocation (after the first N) fails
+//                          (-> temporary exit)
 //   pinned_fail            every pinned host allocation fails (-> pageable)
 //   segv_after_template:N  invalid store once N templates are done (crash report)
 //   slow_template:MS       sleep MS ms per applied template (paces client tests)

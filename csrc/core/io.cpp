@@ -319,4 +319,16 @@ int read_results(const std::string& path, std::vector<ResultLine>& lines, bool& 
   return 0;
 }
 
+int dump_float_buffer(const float* buffer, size_t size, const std::string& path) {
+  FILE* out = std::fopen(path.c_str(), "w");
+  if (!out) {
+    log_message(LOG_ERROR, true, "Error opening file \"%s\" for buffer dump!\n", path.c_str());
+    return RADPUL_EFILE;
+  }
+  for (size_t i = 0; i < size; ++i) std::fprintf(out, "%e\n", buffer[i]);
+  std::fclose(out);
+  log_message(LOG_DEBUG, true, "Successfully wrote buffer to \"%s\"...\n", path.c_str());
+  return 0;
+}
+
 }  // namespace brp

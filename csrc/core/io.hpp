@@ -69,6 +69,10 @@ struct ResultHeaderInfo {
 // Final result file: significance, sort, per-f0 dedupe across harmonics,
 // at most 100 lines, "%DONE%" marker, atomic rename (demod_binary.c:1501-1685).
 // `cands` is modified (fA filled in, powers normalised, sorted).
+// One "%e" value per line, the reference's debug buffer dump
+// (dumpFloatBufferToTextFile, erp_utilities.cpp:216-233).
+int dump_float_buffer(const float* buffer, size_t size, const std::string& path);
+
 int write_results(const std::string& path, CPCand* cands, double t_obs,
                   const ResultHeaderInfo& info);
 

@@ -26,6 +26,7 @@ struct SearchOptions {
   bool prewhitened = false; // series already whitened by another backend (DC removed)
   bool ps_fp16 = false;     // store the power spectrum as fp16 (config 5; needs -W)
   bool device_series = false;  // the whitened series is only needed on the device (no copy back)
+  std::string dump_dir;     // with -z: text dumps of intermediate buffers (reference dumpFloatBufferToTextFile)
 };
 
 // Everything derived from the WU header + options (demod_binary.c:778-782,

@@ -2,6 +2,8 @@
 
 #include <dlfcn.h>
 
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -60,6 +62,25 @@ void range_pop() {
 void mark(const char* name) {
   const Roctx& r = roctx();
   if (r.on && r.mark) r.mark(name);
+}
+
+namespace {
+const auto g_t0 = std::chrono::steady_clock::now();  // static init: ~process start
+}  // namespace
+
+void phase(const char* name) {
+  static const bool on = [] {
+    const char* e = std::getenv("BRP_PHASES");
+    return e && *e && std::strcmp(e, "0") != 0;
+  }();
+  mark(name);
+  if (!on) return;
+  static std::mutex mu;
+  static double prev = 0.0;
+  std::lock_guard<std::mutex> lk(mu);
+  const double t = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - g_t0).count();
+  std::fprintf(stderr, "[phase] %-28s t=%8.1f ms  +%7.1f ms\n", name, t, t - prev);
+  prev = t;
 }
 
 }  // namespace trace

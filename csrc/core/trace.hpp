@@ -15,6 +15,9 @@ bool enabled();
 void range_push(const char* name);
 void range_pop();
 void mark(const char* name);
+// Process phase timeline (BRP_PHASES=1): "name" at milliseconds since process
+// start, and since the previous phase, to stderr; also a roctx mark.
+void phase(const char* name);
 
 struct Range {
   explicit Range(const char* name) : on_(enabled()) {

@@ -48,7 +48,8 @@ class Backend {
                       std::vector<TemplateCands>& out) = 0;
   // Take `first`'s prepared (whitened) series without a host round trip (same
   // device: read in place; another device: peer copy). can_setup_from() is
-  // decided before `first` is set up; setup_from() != 0: not applicable.
+  // decided before `first` is set up; setup_from() == -1: not applicable,
+  // > 0: an error code of the backend (e.g. a device allocation failure).
   virtual bool can_setup_from(const Backend& first, const SearchGeometry& g) const {
     (void)first;
     (void)g;
@@ -57,6 +58,14 @@ class Backend {
   virtual int setup_from(const Backend& first, const SearchGeometry& g) {
     (void)first;
     (void)g;
+    return -1;
+  }
+  // Debug dumps (-z): the prepared series this backend searches and one
+  // template's normalised power spectrum (fft_size bins). -1: not available.
+  virtual int debug_buffers(const TemplateInput& t, std::vector<float>& series, std::vector<float>& ps) {
+    (void)t;
+    (void)series;
+    (void)ps;
     return -1;
   }
   virtual int preferred_batch() const = 0;
@@ -95,8 +104,10 @@ std::unique_ptr<Backend> make_cpu_backend();
 // no-compute backend returning synthetic candidate lists (applier load tests)
 std::unique_ptr<Backend> make_replay_backend(int per_level, int batch);
 // device < 0: auto (BOINC gpu_device_num / first device)
-// True when the HIP pipeline has a compiled FFT plan for this geometry
-// (N even and N/2 = L1*L2*L3 over the compiled lengths, fft_passes.hip).
+// True when the HIP pipeline has an FFT plan for this geometry: the three-pass
+// FFT for N/2 = L1*L2*L3 over the compiled lengths (fft_passes.hip), else the
+// chirp-z transform over such a length (bluestein_kernels.hpp; every N up to
+// 2^31 / 2).
 bool hip_backend_supports(const SearchGeometry& g);
 std::unique_ptr<Backend> make_hip_backend(int device, int batch, int* err);
 // Host waits on HIP work sleep (hipDeviceScheduleBlockingSync) instead of

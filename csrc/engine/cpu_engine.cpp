@@ -39,6 +39,15 @@ class CpuEngine final : public Backend {
     stats_.batches += 1;
     return 0;
   }
+  int debug_buffers(const TemplateInput& t, std::vector<float>& series, std::vector<float>& ps) override {
+    series = series_;
+    const ResampParams p = make_resamp_params(g_.nsamples, g_.n_unpadded, g_.fft_size, g_.dt, g_.step_inv, t.P, t.tau,
+                                              t.Psi0);
+    std::vector<float> x;
+    cpu_resample(series_.data(), p, x, nullptr, nullptr);
+    cpu_power_spectrum(x, g_.fft_size, ps);
+    return 0;
+  }
   int preferred_batch() const override { return 1; }
   // queued submit/complete (Backend defaults), two deep: the search workers'
   // pipelined loop runs on the CPU golden model too

@@ -27,6 +27,7 @@
 #include "../core/log.hpp"
 #include "../core/rngmed.hpp"
 #include "../core/wisdom.hpp"
+#include "../hip/bluestein_kernels.hpp"
 #include "../hip/fft_kernels.hpp"
 #include "../hip/hs_kernels.hpp"
 #include "../hip/resample_kernels.hpp"
@@ -38,11 +39,34 @@ namespace brp {
 
 using hipk::TemplateDev;
 
+namespace {
+constexpr uint64_t kMaxL2L3 = 256ull * 512;  // W_{L2 L3} as lo[256] x hi[512] (build_tables)
+const uint32_t kPlanP3[] = {256, 320, 192, 160, 128, 96, 64};
+const uint32_t kPlanP12[] = {512, 384, 320, 288, 256, 240, 192, 160, 144, 128, 96, 80, 64, 48, 32, 16};
+}  // namespace
+
+// Chirp-z transform of length Mb (bluestein_kernels.hpp): the smallest length
+// L >= 2 Mb - 1 the three-pass FFT factors. The products L1 L2 L3 of the
+// compiled lengths are dense (16 * 2^a 3^b 5^c), so L stays within ~10 % of
+// the minimum.
+bool make_bluestein_plan(uint32_t Mb, FFTPlan3& plan) {
+  const uint64_t need = 2ull * Mb - 1;
+  uint64_t best = 0;
+  for (uint32_t L3 : kPlanP3)
+    for (uint32_t L1 : kPlanP12)
+      for (uint32_t L2 : kPlanP12) {
+        if (L2 > L1 || static_cast<uint64_t>(L2) * L3 > kMaxL2L3 || !hipk::pass12_length_supported(L2)) continue;
+        const uint64_t L = static_cast<uint64_t>(L1) * L2 * L3;
+        if (L >= need && L < (1ull << 31) && (best == 0 || L < best)) best = L;
+      }
+  return best != 0 && make_fft_plan(static_cast<uint32_t>(best), plan);
+}
+
 bool make_fft_plan(uint32_t M, FFTPlan3& plan) {
   plan = FFTPlan3();
   // preference: long pass-3 rows (contiguous PS writes), then balanced L1 >= L2
-  static const uint32_t p3[] = {256, 320, 192, 160, 128, 96, 64};
-  static const uint32_t p12[] = {512, 384, 320, 288, 256, 240, 192, 160, 144, 128, 96, 80, 64, 48, 32, 16};
+  const auto& p3 = kPlanP3;
+  const auto& p12 = kPlanP12;
   for (uint32_t L3 : p3) {
     if (M % L3) continue;
     const uint32_t R = M / L3;
@@ -52,6 +76,7 @@ bool make_fft_plan(uint32_t M, FFTPlan3& plan) {
       const uint32_t L2 = R / L1;
       if (!hipk::pass12_length_supported(L2)) continue;
       if (L1 < L2) continue;
+      if (static_cast<uint64_t>(L2) * L3 > kMaxL2L3) continue;  // pass-2 twiddle table (256 x 512)
       if (!best1 || (L1 - L2) < (best1 - best2)) {
         best1 = L1;
         best2 = L2;
@@ -72,6 +97,18 @@ bool make_fft_plan(uint32_t M, FFTPlan3& plan) {
 
 namespace {
 
+// BRP_FAULT=hip_oom: every device allocation fails; hip_oom:N: the first N
+// succeed (so the first pipeline sets up and a later one fails)
+std::atomic<long> g_device_allocs{0};  // device allocations of this process (fault tests)
+
+bool fault_device_alloc() {
+  const long k = g_device_allocs.fetch_add(1);
+  std::string param;
+  if (!fault_enabled("hip_oom", &param)) return false;
+  const long ok = param.empty() ? 0 : std::atol(param.c_str());
+  return k >= ok;
+}
+
 template <typename T>
 struct DevBuf {
   T* p = nullptr;
@@ -84,7 +121,9 @@ struct DevBuf {
     const hipError_t e = fine ? hipExtMallocWithFlags(reinterpret_cast<void**>(&p), count * sizeof(T),
                                                       hipDeviceMallocFinegrained)
                               : hipMalloc(&p, count * sizeof(T));
-    if (fault_enabled("hip_oom") || e != hipSuccess) {
+    if (fault_device_alloc() || e != hipSuccess) {
+      if (e == hipSuccess) (void)hipFree(p);  // injected failure
+      else (void)hipGetLastError();
       p = nullptr;
       log_message(LOG_ERROR, true, "Couldn't allocate %zu bytes of device memory!\n", count * sizeof(T));
       return RADPUL_HIP_MEM_ALLOC_DEVICE;
@@ -199,6 +238,15 @@ struct HipEngine::Impl {
 
   SearchGeometry g;
   FFTPlan3 plan;
+  // Chirp-z path for lengths the three-pass FFT does not factor: `plan` is
+  // then the length-L plan of the convolution, the DFT has length bs_Mb
+  // (N/2 for even N, N for odd N); bluestein_kernels.hpp
+  bool bs = false;
+  uint32_t bs_Mb = 0;
+  uint32_t bs_nparts = 0;       // chirp-in workgroups per template (partial sums)
+  DevBuf<float2> bs_a;          // [batch][L] chirp-in / convolution spectrum / A
+  DevBuf<float2> bs_h;          // [L] FFT_L of the wrapped conjugate chirp
+  DevBuf<float2> bs_chirp_hi, bs_chirp_lo;  // W_{2 Mb}
   bool ready = false;
   uint32_t num_cus = 256;
   std::string arch;             // gcnArchName (plan-wisdom lookup)
@@ -363,8 +411,118 @@ struct HipEngine::Impl {
     hipk::TwiddleTable t;
     t.hi = tw_hi.p;
     t.lo = tw_lo.p;
-    t.period = 2ull * plan.M * 2ull;  // 2N = 4M
+    t.period = 2ull * g.nsamples;  // W_2N (= W_{4M} of the packed transform)
     return t;
+  }
+  hipk::TwiddleTable chirpt() const {
+    hipk::TwiddleTable t;
+    t.hi = bs_chirp_hi.p;
+    t.lo = bs_chirp_lo.p;
+    t.period = 2ull * bs_Mb;
+    return t;
+  }
+
+  // ---- chirp-z path
+  // y (bs_a) -> FFT_L -> * H, conj (bs_a) -> FFT_L -> conj * w / L = A (bs_a);
+  // pass 2 of the first transform reduces the template partial sums (delta)
+  hipError_t bs_convolve(int nb, bool templates) {
+    hipError_t e = bs_round(nb, 0, templates);
+    return e == hipSuccess ? bs_round(nb, 1, templates) : e;
+  }
+  hipError_t bs_round(int nb, int round, bool templates) {
+    return bs_fft(nb, round == 0 ? hipk::C3_MULCONJ : hipk::C3_CHIRP, bs_a.p, templates && round == 0);
+  }
+  // one length-L transform of bs_a (passes 1, 2 and the epilogue of `mode`
+  // into out); reduce_delta: pass 2 also turns the chirp-in kernel's partial
+  // sums into the per-template padding mean
+  hipError_t bs_fft(int nb, hipk::Pass3CplxMode mode, float2* out, bool reduce_delta) {
+    const hipk::TwiddleTable tw = twt();
+    hipk::Pass1Args a1{};
+    a1.out = buf.p;
+    a1.L2L3 = plan.L2 * plan.L3;
+    a1.L3 = plan.L3;
+    a1.tw = tw;
+    a1.tb = tables();
+    a1.cplx_in = bs_a.p;
+    hipError_t e = hipk::launch_pass1(plan, hipk::P1_COMPLEX, a1, nb, stream);
+    if (e != hipSuccess) return e;
+    hipk::Pass2Args a2{};
+    a2.buf = buf.p;
+    a2.L1 = plan.L1;
+    a2.L2L3 = plan.L2 * plan.L3;
+    a2.L3 = plan.L3;
+    a2.tw = tw;
+    a2.tb = tables();
+    if (reduce_delta) {
+      a2.partials = partials.p;
+      a2.n_partials = bs_nparts;
+      a2.tmpl = tmpl.p;
+      a2.delta = delta.p;
+    }
+    if ((e = hipk::launch_pass2(plan, a2, nb, stream)) != hipSuccess) return e;
+    hipk::Pass3CplxArgs a3{};
+    a3.buf = buf.p;
+    a3.L1 = plan.L1;
+    a3.L2 = plan.L2;
+    a3.L3 = plan.L3;
+    a3.C = plan.L1 * plan.L2;
+    a3.M = plan.M;
+    a3.tb = tables();
+    a3.out = out;
+    a3.out_stride = plan.M;
+    a3.h = bs_h.p;
+    a3.chirp = chirpt();
+    a3.n_out = bs_Mb;
+    a3.scale = static_cast<float>(1.0 / static_cast<double>(plan.M));
+    return hipk::launch_pass3_cplx(plan, mode, a3, nb, stream);
+  }
+  // H = FFT_L of the wrapped conjugate chirp (once per plan)
+  hipError_t bs_make_h() {
+    hipk::BsInArgs a = bs_in();
+    hipError_t e = hipk::launch_bs_chirp_in(hipk::BS_IN_HCHIRP, a, 1, nullptr, stream);
+    return e == hipSuccess ? bs_fft(1, hipk::C3_PLAIN, bs_h.p, false) : e;
+  }
+  hipk::BsInArgs bs_in() const {
+    hipk::BsInArgs a{};
+    a.y = bs_a.p;
+    a.L = plan.M;
+    a.Mb = bs_Mb;
+    a.nsamples = g.nsamples;
+    a.chirp = chirpt();
+    return a;
+  }
+  // template spectra of a batch: resampling + chirp, the two convolution
+  // rounds, power spectrum (bins k < limit into ps_out [nb][stride])
+  hipError_t bs_template_in(int nb, uint32_t* reset) {
+    hipk::BsInArgs a = bs_in();
+    a.series = series_in();
+    a.n_unpadded = g.n_unpadded;
+    a.tmpl = tmpl.p;
+    a.partials = partials.p;
+    a.reset = reset;
+    return hipk::launch_bs_chirp_in(bs_Mb == g.nsamples ? hipk::BS_IN_RESAMPLE1 : hipk::BS_IN_RESAMPLE2, a, nb, nullptr,
+                                    stream);
+  }
+  hipError_t bs_template_power(int nb, float* ps_out, _Float16* ps16_out, uint32_t stride, uint32_t limit) {
+    hipk::BsPowerArgs ap{};
+    ap.A = bs_a.p;
+    ap.L = plan.M;
+    ap.Mb = bs_Mb;
+    ap.nsamples = g.nsamples;
+    ap.tw = twt();
+    ap.limit = limit;
+    ap.ps = ps_out;
+    ap.ps16 = ps16_out;
+    ap.ps_stride = stride;
+    ap.norm = static_cast<float>(1.0 / g.nsamples);
+    ap.tmpl = tmpl.p;
+    ap.delta = delta.p;
+    return hipk::launch_bs_power(ap, nb, stream);
+  }
+  hipError_t bs_template_spectra(int nb, float* ps_out, _Float16* ps16_out, uint32_t stride, uint32_t limit) {
+    hipError_t e = bs_template_in(nb, nullptr);
+    if (e == hipSuccess) e = bs_convolve(nb, true);
+    return e == hipSuccess ? bs_template_power(nb, ps_out, ps16_out, stride, limit) : e;
   }
 
   ~Impl() {
@@ -390,6 +548,7 @@ struct HipEngine::Impl {
         if (fg_in) return hipSuccess;  // the host wrote `in` directly
         return hipMemcpyAsync(in.p, h_in.p, thr_bytes + sizeof(TemplateDev) * nb, hipMemcpyHostToDevice, stream);
       case kPass1: {
+        if (bs) return bs_template_in(nb, &cands.p[0].x);
         hipk::Pass1Args a1{};
         a1.out = buf.p;
         a1.L2L3 = plan.L2 * plan.L3;
@@ -404,6 +563,7 @@ struct HipEngine::Impl {
         return hipk::launch_pass1(plan, hipk::P1_RESAMPLE, a1, nb, stream);
       }
       case kPass2: {
+        if (bs) return bs_round(nb, 0, true);
         hipk::Pass2Args a2{};
         a2.buf = buf.p;
         a2.L1 = plan.L1;
@@ -418,6 +578,12 @@ struct HipEngine::Impl {
         return hipk::launch_pass2(plan, a2, nb, stream);
       }
       case kPass3: {
+        if (bs) {
+          const hipError_t e3 = bs_round(nb, 1, true);
+          if (e3 != hipSuccess) return e3;
+          return bs_template_power(nb, ps.p, ps_fp16 ? reinterpret_cast<_Float16*>(ps.p) : nullptr, ps_stride,
+                                   std::min(g.harmonic_idx_hi, g.fft_size));
+        }
         hipk::Pass3Args a3{};
         a3.buf = buf.p;
         a3.L1 = plan.L1;
@@ -519,7 +685,12 @@ int hip_running_median(int device, const std::vector<float>& in, uint32_t W, std
   int rc;
   const size_t n_out = in.size() - W + 1;
   if ((rc = din.alloc(in.size())) || (rc = dout.alloc(n_out))) return rc;
-  const bool wide = !hipk::running_median_supported(W);
+  bool wide = !hipk::running_median_supported(W);
+  if (!wide && W > 3072) {  // the 128 KB LDS kernel needs a device with that much per workgroup
+    int lds = 0;
+    wide = hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, device < 0 ? 0 : device) != hipSuccess ||
+           lds < 16384 * 8;
+  }
   const uint32_t n_in = static_cast<uint32_t>(in.size());
   if (wide && (rc = scratch.alloc(hipk::running_median_wide_scratch_bytes(n_in)))) return rc;
   auto launch = [&]() {
@@ -644,10 +815,17 @@ int HipEngine::setup_impl(const SearchGeometry& g, const float* host_series, con
   d.g = g;
   d.mu0s.assign(d.slots, 0.0f);
   d.mu0s[0] = mu0;
-  if (g.nsamples % 2 || !make_fft_plan(g.nsamples / 2, d.plan)) {
-    log_message(LOG_ERROR, true, "Unsupported FFT length %u (need N/2 = L1*L2*L3 from the compiled set).\n",
-                g.nsamples);
-    return RADPUL_HIP_FFT_PLAN;
+  d.bs = g.nsamples % 2 != 0 || !make_fft_plan(g.nsamples / 2, d.plan);
+  if (d.bs) {
+    // any other length (every padding -P the reference accepts): chirp-z
+    // transform over the smallest factorable convolution length
+    d.bs_Mb = (g.nsamples % 2) ? g.nsamples : g.nsamples / 2;
+    if (!make_bluestein_plan(d.bs_Mb, d.plan)) {
+      log_message(LOG_ERROR, true, "No FFT plan for length %u.\n", g.nsamples);
+      return RADPUL_HIP_FFT_PLAN;
+    }
+    log_message(LOG_INFO, true, "FFT length %u: chirp-z transform of length %u over %u = %u x %u x %u points.\n",
+                g.nsamples, d.bs_Mb, d.plan.M, d.plan.L1, d.plan.L2, d.plan.L3);
   }
   // measured settings for this (arch, M) from the plan wisdom; environment wins
   const PlanWisdom wis = load_wisdom(wisdom_path(), d.arch, d.plan.M);
@@ -671,7 +849,17 @@ int HipEngine::setup_impl(const SearchGeometry& g, const float* host_series, con
   d.hs_prune = std::getenv("BRP_HS_FULL") == nullptr || std::atoi(std::getenv("BRP_HS_FULL")) == 0;
   d.hs_cell_shift = (std::getenv("BRP_HS_CELL") && std::atoi(std::getenv("BRP_HS_CELL")) == 4) ? 2 : 3;
   if ((rc = d.pyr.alloc(B * hipk::hs_pyr_stride(d.ps_stride)))) return rc;
-  if ((rc = d.partials.alloc(B * d.plan.wg1()))) return rc;
+  d.bs_nparts = d.bs ? hipk::bs_chirp_in_blocks(d.plan.M) : 0;
+  if ((rc = d.partials.alloc(B * std::max(d.plan.wg1(), d.bs_nparts)))) return rc;
+  if (d.bs) {
+    if ((rc = d.bs_a.alloc(B * d.plan.M)) || (rc = d.bs_h.alloc(d.plan.M))) return rc;
+    std::vector<float2> chi, clo;
+    build_twiddles(2ull * d.bs_Mb, chi, clo);
+    if ((rc = d.upload(d.bs_chirp_hi, chi)) || (rc = d.upload(d.bs_chirp_lo, clo))) return rc;
+  } else {
+    d.bs_a.release();
+    d.bs_h.release();
+  }
   if ((rc = d.delta.alloc(B))) return rc;
   if (B > hipk::kHsMaxBatch || g.fundamental_idx_hi >= (1u << hipk::kHsBinBits)) {
     log_message(LOG_ERROR, true, "Batch %zu / fundamental_idx_hi %u beyond the candidate key packing.\n", B,
@@ -724,7 +912,7 @@ int HipEngine::setup_impl(const SearchGeometry& g, const float* host_series, con
   d.io_next = d.io_head = 0;
   d.select_io(0);
   std::vector<float2> hi, lo;
-  build_twiddles(4ull * d.plan.M, hi, lo);
+  build_twiddles(2ull * g.nsamples, hi, lo);
   if ((rc = d.tw_hi.alloc(hi.size()))) return rc;
   if ((rc = d.tw_lo.alloc(lo.size()))) return rc;
   BRP_HIP_CHECK(hipMemcpy(d.tw_hi.p, hi.data(), hi.size() * sizeof(float2), hipMemcpyHostToDevice),
@@ -732,6 +920,10 @@ int HipEngine::setup_impl(const SearchGeometry& g, const float* host_series, con
   BRP_HIP_CHECK(hipMemcpy(d.tw_lo.p, lo.data(), lo.size() * sizeof(float2), hipMemcpyHostToDevice),
                 RADPUL_HIP_MEM_COPY_HOST_DEVICE);
   if ((rc = d.build_tables())) return rc;
+  if (d.bs) {
+    BRP_HIP_CHECK(d.bs_make_h(), RADPUL_HIP_KERNEL_INVOKE);
+    BRP_HIP_CHECK(hipStreamSynchronize(d.stream), RADPUL_HIP_KERNEL_INVOKE);
+  }
   if ((rc = upload_series0(host_series, dev_series, src_device))) return rc;
   log_mem_status(d.device, "after setup");
   d.ready = true;
@@ -835,7 +1027,18 @@ int HipEngine::whiten(const SearchOptions& opt, const std::vector<ZapRange>& zap
   float2* work = d.buf.p;  // M complex scratch (batch slot 0)
   const hipk::TwiddleTable tw = d.twt();
   hipStream_t s = d.stream;
+  const bool odd = (g.nsamples & 1u) != 0;
   // forward r2c of the zero-padded series
+  if (d.bs) {
+    hipk::BsInArgs ab = d.bs_in();
+    ab.real_in = slot_series;
+    ab.n_real = g.n_unpadded;
+    BRP_HIP_CHECK(hipk::launch_bs_chirp_in(odd ? hipk::BS_IN_REAL1 : hipk::BS_IN_REAL2, ab, 1, nullptr, s),
+                  RADPUL_HIP_KERNEL_INVOKE);
+    BRP_HIP_CHECK(d.bs_convolve(1, false), RADPUL_HIP_KERNEL_INVOKE);
+    BRP_HIP_CHECK(hipk::launch_bs_spec(d.bs_a.p, d.bs_Mb, g.nsamples, tw, fft_size, spec.p, s),
+                  RADPUL_HIP_KERNEL_INVOKE);
+  } else {
   hipk::Pass1Args a1{};
   a1.out = work;
   a1.L2L3 = d.plan.L2 * d.plan.L3;
@@ -865,9 +1068,12 @@ int HipEngine::whiten(const SearchOptions& opt, const std::vector<ZapRange>& zap
   a3.limit = fft_size;
   a3.spec = spec.p;
   BRP_HIP_CHECK(hipk::launch_pass3(d.plan, hipk::P3_COMPLEX, a3, 1, s), RADPUL_HIP_KERNEL_INVOKE);
+  }
   BRP_HIP_CHECK(hipk::launch_whiten_power(spec.p, fft_size, psw.p, s), RADPUL_HIP_KERNEL_INVOKE);
-  if (hipk::running_median_supported(opt.window)) {
-    BRP_HIP_CHECK(hipk::launch_running_median(psw.p, fft_size, opt.window, med.p, s), RADPUL_HIP_KERNEL_INVOKE);
+  hipError_t rme = hipErrorInvalidConfiguration;
+  if (hipk::running_median_supported(opt.window)) rme = hipk::launch_running_median(psw.p, fft_size, opt.window, med.p, s);
+  if (rme != hipErrorInvalidConfiguration) {
+    BRP_HIP_CHECK(rme, RADPUL_HIP_KERNEL_INVOKE);
   } else {
     // wide windows (up to the reference's 250 000): device radix sort + median walk
     const size_t bytes = hipk::running_median_wide_scratch_bytes(fft_size);
@@ -912,30 +1118,52 @@ int HipEngine::whiten(const SearchOptions& opt, const std::vector<ZapRange>& zap
     BRP_HIP_CHECK(hipk::launch_zap(spec.p, fft_size, zbins.p, znoise.p, nzu, s), RADPUL_HIP_KERNEL_INVOKE);
   }
   // inverse c2r: tangle, conj-FFT, natural order, scale by 1/sqrt(N), keep n_unpadded
+  const float inv_scale = static_cast<float>(1.0 / std::sqrt(static_cast<float>(g.nsamples)));
   DevBuf<float2>& z = d.w_z;
-  if (z.n < M && (rc = z.alloc(M))) return rc;
-  BRP_HIP_CHECK(hipk::launch_tangle(spec.p, M, fft_size, g.window_2, tw, z.p, s), RADPUL_HIP_KERNEL_INVOKE);
-  a1 = hipk::Pass1Args{};
-  a1.out = work;
-  a1.L2L3 = d.plan.L2 * d.plan.L3;
-  a1.L3 = d.plan.L3;
-  a1.tw = tw;
-  a1.tb = d.tables();
-  a1.cplx_in = z.p;
-  BRP_HIP_CHECK(hipk::launch_pass1(d.plan, hipk::P1_COMPLEX_CONJ, a1, 1, s), RADPUL_HIP_KERNEL_INVOKE);
-  BRP_HIP_CHECK(hipk::launch_pass2(d.plan, a2, 1, s), RADPUL_HIP_KERNEL_INVOKE);
-  hipk::Pass3PlainArgs ap{};
-  ap.buf = work;
-  ap.L1 = d.plan.L1;
-  ap.L2 = d.plan.L2;
-  ap.L3 = d.plan.L3;
-  ap.C = d.plan.L1 * d.plan.L2;
-  ap.tw = tw;
-  ap.tb = d.tables();
-  ap.scale = static_cast<float>(1.0 / std::sqrt(static_cast<float>(g.nsamples)));
-  ap.real_out = slot_series;
-  ap.n_out = g.n_unpadded;
-  BRP_HIP_CHECK(hipk::launch_pass3_plain(d.plan, ap, s), RADPUL_HIP_KERNEL_INVOKE);
+  const uint32_t Mz = d.bs ? d.bs_Mb : M;  // packed half length (even N)
+  if (!odd && z.n < Mz && (rc = z.alloc(Mz))) return rc;
+  if (!odd)
+    BRP_HIP_CHECK(hipk::launch_tangle(spec.p, Mz, fft_size, g.window_2, tw, z.p, s), RADPUL_HIP_KERNEL_INVOKE);
+  if (d.bs) {
+    hipk::BsInArgs ab = d.bs_in();
+    ab.cplx_in = odd ? spec.p : z.p;
+    ab.w2 = g.window_2;
+    ab.fft_size = fft_size;
+    BRP_HIP_CHECK(hipk::launch_bs_chirp_in(odd ? hipk::BS_IN_HERM_CONJ : hipk::BS_IN_CONJ, ab, 1, nullptr, s),
+                  RADPUL_HIP_KERNEL_INVOKE);
+    BRP_HIP_CHECK(d.bs_convolve(1, false), RADPUL_HIP_KERNEL_INVOKE);
+    BRP_HIP_CHECK(hipk::launch_bs_real_out(d.bs_a.p, d.bs_Mb, g.nsamples, inv_scale, slot_series, g.n_unpadded, s),
+                  RADPUL_HIP_KERNEL_INVOKE);
+  } else {
+    hipk::Pass1Args a1{};
+    a1.out = work;
+    a1.L2L3 = d.plan.L2 * d.plan.L3;
+    a1.L3 = d.plan.L3;
+    a1.tw = tw;
+    a1.tb = d.tables();
+    a1.cplx_in = z.p;
+    BRP_HIP_CHECK(hipk::launch_pass1(d.plan, hipk::P1_COMPLEX_CONJ, a1, 1, s), RADPUL_HIP_KERNEL_INVOKE);
+    hipk::Pass2Args a2{};
+    a2.buf = work;
+    a2.L1 = d.plan.L1;
+    a2.L2L3 = d.plan.L2 * d.plan.L3;
+    a2.L3 = d.plan.L3;
+    a2.tw = tw;
+    a2.tb = d.tables();
+    BRP_HIP_CHECK(hipk::launch_pass2(d.plan, a2, 1, s), RADPUL_HIP_KERNEL_INVOKE);
+    hipk::Pass3PlainArgs ap{};
+    ap.buf = work;
+    ap.L1 = d.plan.L1;
+    ap.L2 = d.plan.L2;
+    ap.L3 = d.plan.L3;
+    ap.C = d.plan.L1 * d.plan.L2;
+    ap.tw = tw;
+    ap.tb = d.tables();
+    ap.scale = inv_scale;
+    ap.real_out = slot_series;
+    ap.n_out = g.n_unpadded;
+    BRP_HIP_CHECK(hipk::launch_pass3_plain(d.plan, ap, s), RADPUL_HIP_KERNEL_INVOKE);
+  }
   if (copy_back)
     BRP_HIP_CHECK(hipMemcpyAsync(series.data(), slot_series, g.n_unpadded * sizeof(float), hipMemcpyDeviceToHost, s),
                   RADPUL_HIP_MEM_COPY_DEVICE_HOST);
@@ -1110,6 +1338,18 @@ int HipEngine::power_spectrum(const TemplateInput& t, std::vector<float>& ps_out
                   RADPUL_HIP_MEM_COPY_HOST_DEVICE);
   std::atomic_thread_fence(std::memory_order_seq_cst);
   const hipk::TwiddleTable tw = d.twt();
+  if (d.bs) {
+    DevBuf<float> full;
+    int rc;
+    if ((rc = full.alloc(g.fft_size))) return rc;
+    BRP_HIP_CHECK(d.bs_template_spectra(1, full.p, nullptr, g.fft_size, g.fft_size), RADPUL_HIP_KERNEL_INVOKE);
+    ps_out.resize(g.fft_size);
+    BRP_HIP_CHECK(hipMemcpyAsync(ps_out.data(), full.p, g.fft_size * sizeof(float), hipMemcpyDeviceToHost, s),
+                  RADPUL_HIP_MEM_COPY_DEVICE_HOST);
+    BRP_HIP_CHECK(hipStreamSynchronize(s), RADPUL_HIP_KERNEL_INVOKE);
+    if (n_steps) *n_steps = d.h_tmpl.p[0].n_steps;
+    return 0;
+  }
   hipk::Pass1Args a1{};
   a1.out = d.buf.p;
   a1.L2L3 = d.plan.L2 * d.plan.L3;
@@ -1157,6 +1397,17 @@ int HipEngine::power_spectrum(const TemplateInput& t, std::vector<float>& ps_out
                 RADPUL_HIP_MEM_COPY_DEVICE_HOST);
   BRP_HIP_CHECK(hipStreamSynchronize(s), RADPUL_HIP_KERNEL_INVOKE);
   if (n_steps) *n_steps = d.h_tmpl.p[0].n_steps;
+  return 0;
+}
+
+int HipEngine::download_series(std::vector<float>& series) {
+  Impl& d = *impl_;
+  if (!d.ready || !d.shared_series_valid()) return RADPUL_EMISC;
+  BRP_HIP_CHECK(hipSetDevice(d.device), RADPUL_HIP_DEVICE_SET);
+  BRP_HIP_CHECK(hipStreamSynchronize(d.stream), RADPUL_HIP_KERNEL_INVOKE);
+  series.resize(d.g.n_unpadded);
+  BRP_HIP_CHECK(hipMemcpy(series.data(), d.series_in(), d.g.n_unpadded * sizeof(float), hipMemcpyDeviceToHost),
+                RADPUL_HIP_MEM_COPY_DEVICE_HOST);
   return 0;
 }
 
@@ -1240,9 +1491,9 @@ class HipBackend final : public Backend {
     }
     eng_.set_ps_fp16(opt.ps_fp16);
     int rc = eng_.setup(g, series, static_cast<float>(mean));
-    if (rc) return rc;
-    if (opt.white) return eng_.whiten(opt, zaps, series, 0, !opt.device_series);
-    return 0;
+    if (rc == 0 && opt.white) rc = eng_.whiten(opt, zaps, series, 0, !opt.device_series);
+    log_message(LOG_DEBUG, true, "HIP device allocations so far: %ld\n", g_device_allocs.load());
+    return rc;
   }
   int process(const TemplateInput* t, int n, const float thr[kNumHarmonicLevels],
               std::vector<TemplateCands>& out) override {
@@ -1262,6 +1513,8 @@ class HipBackend final : public Backend {
     const auto* src = dynamic_cast<const HipBackend*>(&first);
     return src != nullptr && src != this;
   }
+  // -1: not applicable; otherwise the engine's error code (an allocation
+  // failure here must still reach the wrapper as a transient resource error)
   int setup_from(const Backend& first, const SearchGeometry& g) override {
     if (!can_setup_from(first, g)) return -1;
     const HipEngine& src = dynamic_cast<const HipBackend&>(first).eng_;
@@ -1269,10 +1522,18 @@ class HipBackend final : public Backend {
     eng_.set_ps_fp16(src.ps_fp16());  // the session's spectrum precision
     const bool force_peer = std::getenv("BRP_PEER_SERIES") != nullptr && std::atoi(std::getenv("BRP_PEER_SERIES")) != 0;
     if (eng_.device() == src.device() && !force_peer) {
-      if (!eng_.prepared_for(g) && eng_.setup_peer(src) != 0) return -1;  // first pass: allocate (D2D copy)
-      return eng_.adopt_series(src) == 0 ? 0 : -1;
+      if (!eng_.prepared_for(g)) {  // first pass: allocate (D2D copy)
+        const int rc = eng_.setup_peer(src);
+        if (rc) return rc;
+      }
+      return eng_.adopt_series(src);
     }
-    return eng_.setup_peer(src) == 0 ? 0 : -1;
+    return eng_.setup_peer(src);
+  }
+  int debug_buffers(const TemplateInput& t, std::vector<float>& series, std::vector<float>& ps) override {
+    int rc = eng_.download_series(series);
+    if (rc == 0) rc = eng_.power_spectrum(t, ps, nullptr);
+    return rc;
   }
   int device() const override { return eng_.device(); }
   int preferred_batch() const override { return eng_.batch(); }
@@ -1293,7 +1554,8 @@ std::shared_ptr<void> hip_pin_host(void* p, size_t bytes) {
 
 bool hip_backend_supports(const SearchGeometry& g) {
   FFTPlan3 p;
-  return g.nsamples % 2 == 0 && make_fft_plan(g.nsamples / 2, p);
+  if (g.nsamples % 2 == 0 && make_fft_plan(g.nsamples / 2, p)) return true;
+  return make_bluestein_plan(g.nsamples % 2 ? g.nsamples : g.nsamples / 2, p);  // chirp-z path
 }
 
 std::unique_ptr<Backend> make_hip_backend(int device, int batch, int* err) {

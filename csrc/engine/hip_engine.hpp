@@ -62,6 +62,8 @@ class HipEngine {
   int max_in_flight() const;
   // test hooks
   int power_spectrum(const TemplateInput& t, std::vector<float>& ps, uint32_t* n_steps);
+  // the (whitened) series of slot 0 as the templates read it
+  int download_series(std::vector<float>& series);
   // time each pipeline stage (prologue, pass1, pass2, pass3, harmonic, epilogue,
   // whole batch) over `reps` back-to-back launches on one batch; microseconds
   int benchmark_stages(const TemplateInput* t, int n, int reps, std::vector<double>& us_per_launch);

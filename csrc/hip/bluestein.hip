@@ -1,0 +1,200 @@
+// Chirp-z (Bluestein) kernels for FFT lengths outside the smooth set (see
+// bluestein_kernels.hpp). The convolution itself runs on the three-pass FFT
+// (fft_passes.hip); these kernels produce its chirp-multiplied input and
+// consume its output.
+#include "bluestein_kernels.hpp"
+#include "fft_block.hpp"
+
+namespace brp {
+namespace hipk {
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kPerThread = 4;  // outputs per thread of the chirp-in kernel
+
+__device__ __forceinline__ float2 chirp_w(const TwiddleTable& t, uint32_t n) {
+  return tw_lookup(t, static_cast<uint64_t>(n) * n);  // W_{2Mb}^{n^2 mod 2Mb}
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(kThreads) bs_chirp_in_kernel(BsInArgs a) {
+  __shared__ float lut_s[kLutSize], lut_c[kLutSize];
+  __shared__ double red[kThreads / kWave + 1];
+  constexpr bool kTemplate = MODE == BS_IN_RESAMPLE2 || MODE == BS_IN_RESAMPLE1;
+  const int b = blockIdx.y;
+  if (a.reset != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *a.reset = 0;
+  TemplateDev td{};
+  const float* series = nullptr;
+  if constexpr (kTemplate) {
+    for (int i = threadIdx.x; i < kLutSize; i += kThreads) {
+      lut_s[i] = kSinLut[i];
+      lut_c[i] = kCosLut[i];
+    }
+    __syncthreads();
+    td = a.tmpl[b];
+    series = a.series + static_cast<size_t>(td.wu) * a.n_unpadded;
+  }
+  const bool fast = a.n_unpadded <= (1u << 23);
+  const int last = static_cast<int>(a.n_unpadded) - 1;
+  // centred resampled sample m (zero beyond n_steps: the mean padding is
+  // added analytically in bs_power_kernel)
+  auto sample = [&](uint32_t m) -> float {
+    if (m >= td.n_steps) return 0.0f;
+    const float dt = resamp_del_t(m, td.p, lut_s, lut_c);
+    const int i = min(max(fast ? resamp_nearest_f(m, dt) : resamp_nearest(m, dt), 0), last);
+    return series[i] - td.mu0;
+  };
+  float fsum = 0.0f;
+  float2* y = a.y + static_cast<size_t>(b) * a.L;
+  const uint32_t n0 = (blockIdx.x * kPerThread) * kThreads + threadIdx.x;
+#pragma unroll
+  for (int u = 0; u < kPerThread; ++u) {
+    const uint32_t n = n0 + u * kThreads;
+    if (n >= a.L) break;
+    float2 v = make_float2(0.0f, 0.0f);
+    if (MODE == BS_IN_HCHIRP) {
+      // h_n = conj(w_n) for n < Mb, h_{L-n} = conj(w_n) for 0 < n < Mb
+      if (n < a.Mb) v = conjf2(chirp_w(a.chirp, n));
+      else if (a.L - n < a.Mb) v = conjf2(chirp_w(a.chirp, a.L - n));
+    } else if (n < a.Mb) {
+      float2 x;
+      if (MODE == BS_IN_RESAMPLE2) {
+        x = make_float2(sample(2 * n), sample(2 * n + 1));
+        fsum += x.x + x.y;
+      } else if (MODE == BS_IN_RESAMPLE1) {
+        x = make_float2(sample(n), 0.0f);
+        fsum += x.x;
+      } else if (MODE == BS_IN_REAL2) {
+        x = make_float2(2 * n < a.n_real ? a.real_in[2 * n] : 0.0f, 2 * n + 1 < a.n_real ? a.real_in[2 * n + 1] : 0.0f);
+      } else if (MODE == BS_IN_REAL1) {
+        x = make_float2(n < a.n_real ? a.real_in[n] : 0.0f, 0.0f);
+      } else if (MODE == BS_IN_CONJ) {
+        x = conjf2(a.cplx_in[n]);
+      } else {  // BS_IN_HERM_CONJ: F_n = X_n (n <= (N-1)/2), conj(X_{N-n}) above; input conj(F_n)
+        // with the whitening's zeroed edges and Im X_0 = 0 (c2r semantics, as tangle_kernel)
+        auto bin = [&](uint32_t q) -> float2 {
+          if (q < a.w2 || q >= a.fft_size - a.w2) return make_float2(0.0f, 0.0f);
+          float2 v = a.cplx_in[q];
+          if (q == 0) v.y = 0.0f;
+          return v;
+        };
+        const uint32_t half = (a.nsamples - 1) / 2;
+        x = n <= half ? conjf2(bin(n)) : bin(a.nsamples - n);
+      }
+      v = cmul(x, chirp_w(a.chirp, n));
+    }
+    y[n] = v;
+  }
+  if constexpr (kTemplate) {
+    const double tot = block_sum<kThreads>(static_cast<double>(fsum), red);
+    if (threadIdx.x == 0) a.partials[static_cast<size_t>(b) * gridDim.x + blockIdx.x] = tot;
+  }
+}
+
+// X_k of the real transform from the length-Mb DFT A: even N (A = DFT of the
+// packed pairs, Mb = N/2): untangle A_k, A_{Mb-k}; odd N (A = DFT of the real
+// series, Mb = N): X_k = A_k for k <= (N-1)/2 and the DFT's own symmetric value
+// conj(A_{N-k}) at k = (N+1)/2 (the one bin fft_size reaches beyond it)
+__device__ __forceinline__ float2 bs_bin(const float2* A, uint32_t Mb, uint32_t N, const TwiddleTable& tw, uint32_t k) {
+  if (N & 1u) {
+    const uint32_t half = (N - 1) / 2;
+    return k <= half ? A[k] : conjf2(A[N - k]);
+  }
+  if (k == Mb) return make_float2(A[0].x - A[0].y, 0.0f);  // Nyquist
+  const float2 zk = A[k], zm = A[(Mb - k) % Mb];
+  return untangle_w(zk, zm, tw_lookup(tw, 2ull * k));  // W_N^k = W_2N^{2k}
+}
+
+template <bool HALF>
+__global__ void __launch_bounds__(kThreads) bs_power_kernel(BsPowerArgs a) {
+  const int b = blockIdx.y;
+  const uint32_t k = blockIdx.x * kThreads + threadIdx.x;
+  if (k >= a.limit) return;
+  float p = 0.0f;
+  const uint32_t real_bins = a.nsamples / 2 + 1;  // bins the real DFT defines
+  if (k > 0 && k < real_bins) {
+    const float2* A = a.A + static_cast<size_t>(b) * a.L;
+    float2 x = bs_bin(A, a.Mb, a.nsamples, a.tw, k);
+    const uint32_t n_s = a.tmpl[b].n_steps;
+    if (n_s > 0) {  // + delta * S_k, S_k the transform of the padding indicator
+      const float dS = static_cast<float>(a.delta[b]);
+      const float2 tk = tw_lookup(a.tw, k);
+      const float2 ta = tw_lookup(a.tw, static_cast<uint64_t>(n_s) * k);
+      const float2 sp = padding_spectrum_t(ta, tk, cmul(ta, conjf2(tk)));  // tc = W_2N^{(n_s - 1) k}
+      x = make_float2(x.x + dS * sp.x, x.y + dS * sp.y);
+    }
+    p = (x.x * x.x + x.y * x.y) * a.norm;
+  }
+  const size_t o = static_cast<size_t>(b) * a.ps_stride + k;
+  if (HALF) a.ps16[o] = static_cast<_Float16>(p);
+  else a.ps[o] = p;
+}
+
+__global__ void __launch_bounds__(kThreads) bs_spec_kernel(const float2* A, uint32_t Mb, uint32_t N, TwiddleTable tw,
+                                                           uint32_t fft_size, float2* spec) {
+  const uint32_t k = blockIdx.x * kThreads + threadIdx.x;
+  if (k < fft_size) spec[k] = bs_bin(A, Mb, N, tw, k);
+}
+
+// inverse transforms: A = DFT(conj(input)); even N: the packed pairs
+// conj(A_n) -> (x[2n], x[2n+1]); odd N: x[n] = Re A_n
+__global__ void __launch_bounds__(kThreads) bs_real_out_kernel(const float2* A, uint32_t Mb, uint32_t N, float scale,
+                                                               float* out, uint32_t n_out) {
+  const uint32_t n = blockIdx.x * kThreads + threadIdx.x;
+  if (n >= Mb) return;
+  const float2 v = A[n];
+  if (N & 1u) {
+    if (n < n_out) out[n] = v.x * scale;
+  } else {
+    if (2 * n < n_out) out[2 * n] = v.x * scale;
+    if (2 * n + 1 < n_out) out[2 * n + 1] = -v.y * scale;
+  }
+}
+
+}  // namespace
+
+uint32_t bs_chirp_in_blocks(uint32_t L) { return (L + kThreads * kPerThread - 1) / (kThreads * kPerThread); }
+
+hipError_t launch_bs_chirp_in(BsInMode mode, const BsInArgs& a, int batch, uint32_t* n_partials, hipStream_t s) {
+  const dim3 grid(bs_chirp_in_blocks(a.L), batch);
+  if (n_partials) *n_partials = grid.x;
+  switch (mode) {
+#define BRP_BS_CASE(M) \
+  case M: hipLaunchKernelGGL((bs_chirp_in_kernel<M>), grid, dim3(kThreads), 0, s, a); break;
+    BRP_BS_CASE(BS_IN_RESAMPLE2)
+    BRP_BS_CASE(BS_IN_RESAMPLE1)
+    BRP_BS_CASE(BS_IN_REAL2)
+    BRP_BS_CASE(BS_IN_REAL1)
+    BRP_BS_CASE(BS_IN_CONJ)
+    BRP_BS_CASE(BS_IN_HERM_CONJ)
+    BRP_BS_CASE(BS_IN_HCHIRP)
+#undef BRP_BS_CASE
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_bs_power(const BsPowerArgs& a, int batch, hipStream_t s) {
+  const dim3 grid((a.limit + kThreads - 1) / kThreads, batch);
+  if (a.ps16) hipLaunchKernelGGL((bs_power_kernel<true>), grid, dim3(kThreads), 0, s, a);
+  else hipLaunchKernelGGL((bs_power_kernel<false>), grid, dim3(kThreads), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_bs_spec(const float2* A, uint32_t Mb, uint32_t nsamples, const TwiddleTable& tw, uint32_t fft_size,
+                          float2* spec, hipStream_t s) {
+  hipLaunchKernelGGL(bs_spec_kernel, dim3((fft_size + kThreads - 1) / kThreads), dim3(kThreads), 0, s, A, Mb,
+                     nsamples, tw, fft_size, spec);
+  return hipGetLastError();
+}
+
+hipError_t launch_bs_real_out(const float2* A, uint32_t Mb, uint32_t nsamples, float scale, float* out,
+                              uint32_t n_out, hipStream_t s) {
+  hipLaunchKernelGGL(bs_real_out_kernel, dim3((Mb + kThreads - 1) / kThreads), dim3(kThreads), 0, s, A, Mb, nsamples,
+                     scale, out, n_out);
+  return hipGetLastError();
+}
+
+}  // namespace hipk
+}  // namespace brp

@@ -40,6 +40,7 @@ enum Pass1Mode : int {
   P1_RESAMPLE = 0,   // fused nearest-neighbour resampling of the time series
   P1_REAL = 1,       // zero-padded real series
   P1_COMPLEX_CONJ = 2,  // complex input, conjugated (inverse transform)
+  P1_COMPLEX = 3,       // complex input as is (chirp-z convolutions, bluestein_kernels.hpp)
 };
 
 struct Pass1Args {
@@ -56,7 +57,7 @@ struct Pass1Args {
   // P1_REAL
   const float* real_in;
   uint32_t n_real;
-  // P1_COMPLEX_CONJ
+  // P1_COMPLEX_CONJ, P1_COMPLEX: [batch][M]
   const float2* cplx_in;
 };
 

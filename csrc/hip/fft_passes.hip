@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <type_traits>
 
+#include "bluestein_kernels.hpp"
 #include "fft_block.hpp"
 #include "fft_kernels.hpp"
 
@@ -121,7 +122,8 @@ __global__ void __launch_bounds__(kNcol * tpc_for<L>()) pass1_kernel(Pass1Args a
   } else {
     for (int r = tj; r < L; r += TPC) {
       const uint32_t n = r * a.L2L3 + col_base + c;
-      data[Lay::idx(r, c)] = conjf2(a.cplx_in[static_cast<size_t>(b) * M + n]);
+      const float2 v = a.cplx_in[static_cast<size_t>(b) * M + n];
+      data[Lay::idx(r, c)] = MODE == P1_COMPLEX_CONJ ? conjf2(v) : v;
     }
   }
   copy_stage_twiddles<L>(twl, a.tb.st1);
@@ -688,6 +690,49 @@ __global__ void __launch_bounds__(ROWS * tpc_for<L>()) pass3_plain_kernel(Pass3P
   }
 }
 
+// Row pass of the chirp-z convolutions (bluestein_kernels.hpp): L3-point row
+// FFTs of ROWS rows, natural-order complex output n = c + C k3 with the
+// convolution's pointwise epilogue fused (multiply by H and conjugate, or the
+// final chirp and 1/L), batched over blockIdx.y.
+template <int L, int ROWS, int MODE>
+__global__ void __launch_bounds__(ROWS * tpc_for<L>()) pass3_cplx_kernel(Pass3CplxArgs a) {
+  constexpr int TPC = tpc_for<L>();
+  constexpr int NT = ROWS * TPC;
+  using Lay = BlockLayout<L, ROWS, TPC, true>;
+  __shared__ __attribute__((aligned(16))) float2 smem[Lay::kLds + kTwPad<L>];
+  float2* data = smem;
+  float2* twl = smem + Lay::kLds;
+  const int b = blockIdx.y;
+  const uint32_t c0 = blockIdx.x * ROWS;
+  const float2* buf = a.buf + static_cast<size_t>(b) * a.M;
+  {
+    int slot, tj;
+    Lay::coords(threadIdx.x, slot, tj);
+    const float2* src = buf + row_base(c0 + slot, a.L1, a.L2, a.L3);
+    for (int r = tj; r < L; r += TPC) data[Lay::idx(r, slot)] = src[r];
+  }
+  copy_stage_twiddles<L>(twl, a.tb.st3);
+  __syncthreads();
+  BlockFFT<L, ROWS, TPC, true>::run(data, twl);
+  const int s = threadIdx.x % ROWS;
+  const int t = threadIdx.x / ROWS;
+  constexpr int kStreams = NT / ROWS;
+  const uint32_t c = c0 + s;
+  float2* out = a.out + static_cast<size_t>(b) * a.out_stride;
+  for (int k3 = t; k3 < L; k3 += kStreams) {
+    const float2 z = data[Lay::idx(k3, s)];
+    const uint32_t n = c + a.C * static_cast<uint32_t>(k3);
+    if (MODE == C3_PLAIN) {
+      out[n] = z;
+    } else if (MODE == C3_MULCONJ) {
+      out[n] = conjf2(cmul(z, a.h[n]));
+    } else if (n < a.n_out) {
+      const float2 w = tw_lookup(a.chirp, static_cast<uint64_t>(n) * n);
+      out[n] = cscale(cmul(conjf2(z), w), a.scale);
+    }
+  }
+}
+
 }  // namespace
 
 // ------------------------------------------------------------ dispatch glue
@@ -736,6 +781,7 @@ hipError_t launch_pass1(const FFTPlan3& plan, Pass1Mode mode, const Pass1Args& a
     const dim3 block(kNcol * tpc_for<n>());                                                           \
     if (mode == P1_RESAMPLE) hipLaunchKernelGGL((pass1_kernel<n, P1_RESAMPLE>), grid, block, 0, s, a); \
     else if (mode == P1_REAL) hipLaunchKernelGGL((pass1_kernel<n, P1_REAL>), grid, block, 0, s, a);    \
+    else if (mode == P1_COMPLEX) hipLaunchKernelGGL((pass1_kernel<n, P1_COMPLEX>), grid, block, 0, s, a); \
     else hipLaunchKernelGGL((pass1_kernel<n, P1_COMPLEX_CONJ>), grid, block, 0, s, a);                 \
     break;                                                                                            \
   }
@@ -786,6 +832,25 @@ hipError_t launch_pass3(const FFTPlan3& plan, Pass3Mode mode, const Pass3Args& a
     else if (mode == P3_POWER) hipLaunchKernelGGL((pass3_kernel<n, kRows3, P3_POWER>), grid, block, 0, s, a); \
     else hipLaunchKernelGGL((pass3_kernel<n, kRows3, P3_COMPLEX>), grid, block, 0, s, a);                 \
     break;                                                                                                \
+  }
+    BRP_P3_LENGTHS(X)
+#undef X
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_pass3_cplx(const FFTPlan3& plan, Pass3CplxMode mode, const Pass3CplxArgs& a, int batch,
+                             hipStream_t s) {
+  const dim3 grid(plan.wg3_plain(), batch);
+  switch (plan.L3) {
+#define X(n)                                                                                                       \
+  case n: {                                                                                                        \
+    const dim3 block(kRows3 * tpc_for<n>());                                                                       \
+    if (mode == C3_PLAIN) hipLaunchKernelGGL((pass3_cplx_kernel<n, kRows3, C3_PLAIN>), grid, block, 0, s, a);     \
+    else if (mode == C3_MULCONJ) hipLaunchKernelGGL((pass3_cplx_kernel<n, kRows3, C3_MULCONJ>), grid, block, 0, s, a); \
+    else hipLaunchKernelGGL((pass3_cplx_kernel<n, kRows3, C3_CHIRP>), grid, block, 0, s, a);                     \
+    break;                                                                                                         \
   }
     BRP_P3_LENGTHS(X)
 #undef X

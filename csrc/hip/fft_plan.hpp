@@ -32,5 +32,8 @@ struct FFTPlan3 {
 // Chooses lengths from the instantiated kernel set; returns false if M is not
 // supported (non-smooth length).
 bool make_fft_plan(uint32_t M, FFTPlan3& plan);
+// Plan of the convolution of a chirp-z transform of length Mb (any Mb): the
+// smallest supported L >= 2 Mb - 1 (bluestein_kernels.hpp).
+bool make_bluestein_plan(uint32_t Mb, FFTPlan3& plan);
 
 }  // namespace brp

@@ -243,14 +243,17 @@ constexpr int kHarm[16] = {16, 8, 12, 4, 14, 10, 6, 2, 15, 13, 11, 9, 7, 5, 3, 1
 template <int CK>
 struct HsStage {
   static constexpr int lvl(int l) { return l >= 4 ? CK : 0; }
-  static constexpr int wave_cells(int l) { return (((l * (kWaveSpan - 1) + 15) / 16) >> lvl(l)) + 2; }
+  // cells of harmonic l the wave's blocks reach, counted from the wave's first
+  // cell rounded down to even (so that cell pairs are 8-byte aligned in LDS)
+  static constexpr int wave_cells(int l) { return (((l * (kWaveSpan - 1) + 15) / 16) >> lvl(l)) + 3; }
+  static constexpr int slice_len(int l) { return (wave_cells(l) + 1) & ~1; }
   static constexpr int slice(int q) {
     int o = 0;
-    for (int r = 0; r < q; ++r) o += wave_cells(kHarm[r]);
+    for (int r = 0; r < q; ++r) o += slice_len(kHarm[r]);
     return o;
   }
-  static constexpr int kCells = slice(16);
-  static constexpr int chunks(int q) { return (wave_cells(kHarm[q]) + kWave - 1) / kWave; }
+  static constexpr int kCells = slice(16) + 8;  // pair reads past a slice end stay inside the buffer
+  static constexpr int chunks(int q) { return (slice_len(kHarm[q]) + kWave - 1) / kWave; }
   static constexpr int chunk0(int q) {
     int o = 0;
     for (int r = 0; r < q; ++r) o += chunks(r);
@@ -273,7 +276,7 @@ __device__ __forceinline__ void hs_load(float* v, const T* P, const float* C8, u
   using S = HsStage<CK>;
   constexpr int L = kHarm[Q], K = S::lvl(L);
   const uint32_t lim = K ? n8 : nps;
-  const uint32_t c0 = hs_cell(L, K, I0);
+  const uint32_t c0 = hs_cell(L, K, I0) & ~1u;
 #pragma unroll
   for (int q = 0; q < S::chunks(Q); ++q) {
     const uint32_t c = c0 + static_cast<uint32_t>(lane + kWave * q);
@@ -285,7 +288,7 @@ __device__ __forceinline__ void hs_load(float* v, const T* P, const float* C8, u
 template <int CK, int Q>
 __device__ __forceinline__ void hs_store(float* buf, const float* v, int lane) {
   using S = HsStage<CK>;
-  constexpr int N = S::wave_cells(kHarm[Q]);
+  constexpr int N = S::slice_len(kHarm[Q]);
 #pragma unroll
   for (int q = 0; q < S::chunks(Q); ++q) {
     const int e = lane + kWave * q;
@@ -299,7 +302,7 @@ __device__ __forceinline__ float hs_span_max(const float* buf, int32_t I0, int32
   using S = HsStage<CK>;
   constexpr int L = kHarm[Q], K = S::lvl(L);
   constexpr int kCells = (((L * (N - 1) + 15) / 16) >> K) + 2;
-  const float* s = buf + S::slice(Q) - hs_cell(L, K, I0);
+  const float* s = buf + S::slice(Q) - (hs_cell(L, K, I0) & ~1u);
   const uint32_t lo = hs_cell(L, K, i), hi = hs_cell(L, K, i + N - 1);
   float m = s[lo];
 #pragma unroll
@@ -329,23 +332,135 @@ __device__ __forceinline__ void hs_tail_max(std::integer_sequence<int, Q...>, co
   ((m[Q] = fmaxf(m[Q], hs_span_max<CK, Q, kBlkSpan - kBlk>(buf, I0, i))), ...);
 }
 
+// Maxima of harmonic kHarm[Q] over the block's 16 indices (m16) and, for the
+// first 8 harmonics, over its 20-index reach (m20), read as aligned cell pairs
+// (ds_read_b64). A 32-lane group of b64 reads is serviced by 64 banks, and the
+// pairs lanes request advance by L/16 <= 1 per lane (8-bin cells), so the reads
+// are conflict free; b32 reads of the same cells advance by L/8 > 1 words per
+// lane for L > 8 and collided 2-way (profiles/pmc_bytes_pruned_hs_r2.txt: 62 %
+// of the kernel's LDS cycles were bank conflicts). Cells outside [lo, hi] of
+// the loaded pairs are masked, so the maxima (and the bounds) are exactly
+// those of hs_span_max. Harmonic 3 reads spectrum words at a stride of 3 per
+// lane: b32 reads are already conflict free there (pairs would not be).
+template <int CK, int Q>
+__device__ __forceinline__ void hs_pair_max(const float* buf, int32_t I0, int32_t ib, float& m16, float& m20) {
+  using S = HsStage<CK>;
+  constexpr int L = kHarm[Q], K = S::lvl(L);
+  constexpr bool kTail = Q < 8;
+  if constexpr (L == 3) {
+    m16 = m20 = hs_span_max<CK, Q, kBlk>(buf, I0, ib);
+  } else {
+    constexpr int N = kTail ? kBlkSpan : kBlk;
+    constexpr int kSpan = (((L * (N - 1) + 15) / 16) >> K) + 2;  // hi - lo < kSpan
+    constexpr int NP = kSpan / 2 + 1;                              // pairs covering [lo & ~1, lo + kSpan)
+    const float ninf = -__builtin_inff();
+    const uint32_t cb = hs_cell(L, K, I0) & ~1u;
+    const uint32_t lo = hs_cell(L, K, ib), h16 = hs_cell(L, K, ib + kBlk - 1);
+    const uint32_t h20 = kTail ? hs_cell(L, K, ib + kBlkSpan - 1) : h16;
+    // volatile: keeps each pair read a ds_read_b64 (the load-store optimiser
+    // would merge neighbours into ds_read2_b64, serviced as 32 banks / 4 x 16
+    // lanes at twice the cycles)
+    using f2 = float __attribute__((ext_vector_type(2)));
+    using lds_f2 = const volatile f2 __attribute__((address_space(3)))*;
+    const lds_f2 s = (lds_f2)(buf + S::slice(Q)) + ((lo - cb) >> 1);
+    const uint32_t c0 = lo & ~1u;
+    // cells c0 + e with e <= kIn lie in [lo, h16] for every block: since
+    // (x + y) >> 4 >= (x >> 4) + (y >> 4), h16 - lo >= (15 L / 16) >> K
+    constexpr int kIn = ((15 * L) / 16) >> K;
+    float a = ninf, t = ninf;
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+      const f2 v = s[j];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int i = 2 * j + e;
+        float x = e ? v.y : v.x;
+        if (i == 0) x = (lo & 1u) ? ninf : x;
+        if (i <= kIn) {
+          a = fmaxf(a, x);
+        } else {
+          const uint32_t c = c0 + static_cast<uint32_t>(i);
+          a = fmaxf(a, c <= h16 ? x : ninf);
+          if constexpr (kTail) t = fmaxf(t, c <= h20 ? x : ninf);
+        }
+      }
+    }
+    t = fmaxf(a, t);
+    m16 = a;
+    m20 = kTail ? t : a;
+  }
+}
+
 template <int CK, int... Q>
 __device__ __forceinline__ void hs_bounds(std::integer_sequence<int, Q...>, const float* buf, int32_t I0,
                                           int32_t ib, float* u) {
-  const float m16[16] = {hs_span_max<CK, Q, kBlk>(buf, I0, ib)...};
-  float m20[8];
+  if constexpr (CK == 3) {
+    // running sums in the reference order, harmonic by harmonic; each group's
+    // partial sums are pinned (empty volatile asm) before the next group's
+    // volatile pair reads, so the reads of one group die before the next are
+    // issued (all 33 hoisted ahead of their uses held 120 VGPRs: 4 instead of
+    // 5 waves per SIMD)
+    float m16, m20, x16, x20;
+    auto hm = [&](auto qc, float& a16, float& a20) {
+      hs_pair_max<CK, decltype(qc)::value>(buf, I0, ib, a16, a20);
+    };
+    using std::integral_constant;
+    auto pin = [](float& p, float& q) { asm volatile("" : "+v"(p), "+v"(q)); };
+    hm(integral_constant<int, 0>{}, m16, m20);
+    u[0] = m20;
+    float v = m16;
+    hm(integral_constant<int, 1>{}, m16, m20);
+    u[1] = u[0] + m20;
+    v += m16;
+    pin(u[1], v);
+    hm(integral_constant<int, 2>{}, m16, m20);
+    hm(integral_constant<int, 3>{}, x16, x20);
+    u[2] = u[1] + (m20 + x20);
+    v += m16 + x16;
+    pin(u[2], v);
+    hm(integral_constant<int, 4>{}, m16, m20);
+    hm(integral_constant<int, 5>{}, x16, x20);
+    float s20 = m20 + x20, s16 = m16 + x16;
+    pin(s20, s16);
+    hm(integral_constant<int, 6>{}, m16, m20);
+    hm(integral_constant<int, 7>{}, x16, x20);
+    u[3] = u[2] + ((s20 + m20) + x20);
+    v += (s16 + m16) + x16;
+    pin(u[3], v);
+    hm(integral_constant<int, 8>{}, m16, m20);
+    hm(integral_constant<int, 9>{}, x16, x20);
+    float w = m16 + x16;
+    pin(w, v);
+    hm(integral_constant<int, 10>{}, m16, m20);
+    hm(integral_constant<int, 11>{}, x16, x20);
+    w = (w + m16) + x16;
+    pin(w, v);
+    hm(integral_constant<int, 12>{}, m16, m20);
+    hm(integral_constant<int, 13>{}, x16, x20);
+    w = (w + m16) + x16;
+    pin(w, v);
+    hm(integral_constant<int, 14>{}, m16, m20);
+    hm(integral_constant<int, 15>{}, x16, x20);
+    w = (w + m16) + x16;
+    u[4] = v + w;
+    (void)m20;
+    (void)x20;
+  } else {  // 4-bin cells (switch): pair strides of 2 would collide; b32 reads
+    const float m16[16] = {hs_span_max<CK, Q, kBlk>(buf, I0, ib)...};
+    float m20[8];
 #pragma unroll
-  for (int q = 0; q < 8; ++q) m20[q] = m16[q];
-  hs_tail_max<CK>(std::make_integer_sequence<int, 8>{}, buf, I0, ib + kBlk, m20);
-  u[0] = m20[0];
-  u[1] = u[0] + m20[1];
-  u[2] = u[1] + (m20[2] + m20[3]);
-  u[3] = u[2] + (((m20[4] + m20[5]) + m20[6]) + m20[7]);
-  float v = m16[0];
-  v += m16[1];
-  v += m16[2] + m16[3];
-  v += ((m16[4] + m16[5]) + m16[6]) + m16[7];
-  u[4] = v + (((((((m16[8] + m16[9]) + m16[10]) + m16[11]) + m16[12]) + m16[13]) + m16[14]) + m16[15]);
+    for (int q = 0; q < 8; ++q) m20[q] = m16[q];
+    hs_tail_max<CK>(std::make_integer_sequence<int, 8>{}, buf, I0, ib + kBlk, m20);
+    u[0] = m20[0];
+    u[1] = u[0] + m20[1];
+    u[2] = u[1] + (m20[2] + m20[3]);
+    u[3] = u[2] + (((m20[4] + m20[5]) + m20[6]) + m20[7]);
+    float v = m16[0];
+    v += m16[1];
+    v += m16[2] + m16[3];
+    v += ((m16[4] + m16[5]) + m16[6]) + m16[7];
+    u[4] = v + (((((((m16[8] + m16[9]) + m16[10]) + m16[11]) + m16[12]) + m16[13]) + m16[14]) + m16[15]);
+  }
 }
 
 // One thread per 16-index block computes the bounds; the wave then computes
@@ -358,7 +473,7 @@ template <int CK, int MODE>
 __global__ void __launch_bounds__(256) hs_pruned_kernel(HSArgs a, uint32_t nblk) {
 #pragma clang fp contract(off)
   constexpr int kSubs = kWave / kBlkSpan;  // 3
-  __shared__ float stage[4][HsStage<CK>::kCells];
+  __shared__ __attribute__((aligned(16))) float stage[4][HsStage<CK>::kCells];
   __shared__ float sv[4][kSubs][4][kBlkSpan];
   const int b = blockIdx.y;
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;

@@ -193,6 +193,14 @@ hipError_t launch_running_median(const float* in, uint32_t n_in, uint32_t W, flo
   if (!running_median_supported(W) || n_in < W) return hipErrorInvalidValue;
   const uint32_t n_out = n_in - W + 1;
   if (W > 3072) {
+    // 128 KB of static LDS per workgroup: gfx950 has 160 KB per CU; on a
+    // device with less, the wide-window path (rmed_wide.hip) serves these W
+    int dev = 0;
+    int lds = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess ||
+        lds < 16384 * 8)
+      return hipErrorInvalidConfiguration;
     constexpr int kSpanL = 16384, kThreadsL = 1024;
     const uint32_t perL = kSpanL - W + 1;
     hipLaunchKernelGGL((running_median_kernel<kSpanL, kThreadsL, true>), dim3((n_out + perL - 1) / perL),

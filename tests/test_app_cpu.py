@@ -171,14 +171,19 @@ def test_shmem_xml_render(brp):
     assert m is not None and len(m.group(1)) == 80
 
 
-def test_unsupported_fft_length_falls_back_to_cpu(brp, case, tmp_path):
-    # padding 1.3 -> N/2 has a prime factor the HIP FFT is not compiled for:
-    # the session switches to the CPU golden model (with a warning) instead of failing
-    cfg = _cfg(case, tmp_path, padding=1.3, use_cpu=False)
+def test_any_padding_has_a_device_plan_and_runs_on_the_golden_model(brp, case, tmp_path):
+    # padding 1.3 -> N/2 has a prime factor outside the three-pass FFT's
+    # lengths: the HIP backend takes the chirp-z path (no CPU fallback in the
+    # product path; GPU parity in tests/test_gpu_bluestein.py), and the CPU
+    # golden model (chirp-z double FFT for such lengths) searches it too
+    from boinc_app_eah_brp_amd import ops
+
+    cfg = _cfg(case, tmp_path, padding=1.3, use_cpu=True)
     out = BRPSearch(cfg).run(end=3, write_output=False, use_checkpoint=False)
     assert out.templates_run == 3
-    M = out.geometry["nsamples"] // 2
-    assert brp.fft_plan(M) is None
+    N = out.geometry["nsamples"]
+    assert brp.fft_plan(N // 2) is None
+    assert ops.fft_path(N).kind == "chirp-z"
 
 
 def test_app_mi355x_flags_parse(app, case, tmp_path):

@@ -62,6 +62,16 @@ def test_graphics_shared_memory_file(app, small, tmp_path):
     assert "<graphics_info>" in xml and "<fraction_done>" in xml and "<dispersion>" in xml
 
 
+def test_graphics_shared_memory_named_after_slot(app, small, tmp_path):
+    """libboinc names the graphics segment boinc_<app>_<slot> after
+    init_data.xml's slot (erp_boinc_ipc.cpp:188 via boinc_graphics_make_shmem)."""
+    (tmp_path / "init_data.xml").write_text("<app_init_data>\n<slot>3</slot>\n</app_init_data>\n")
+    r = _run(app, _args(small, tmp_path / "r.cand", tmp_path / "c.cpt"), tmp_path)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert (tmp_path / "boinc_EinsteinRadio_3").exists()
+    assert not (tmp_path / "boinc_EinsteinRadio_0").exists()
+
+
 def test_multi_pass_wrapper(app, small, tmp_path):
     # two -i/-o pairs processed as sequential passes; the checkpoint is removed after each
     args = ["-i", small["wu"], "-o", str(tmp_path / "a.cand"), "-i", small["wu"], "-o", str(tmp_path / "b.cand"),
@@ -103,3 +113,28 @@ def test_app_info_template_is_valid():
     assert av.find("coproc/type").text == "ATI"
     assert av.find("file_ref/file_name").text == root.find("file_info/name").text
     assert av.find("cmdline").text.split()[0] == "--mi355x-pipelines"
+
+
+def test_debug_buffer_dumps(app, small, tmp_path):
+    """-z with --mi355x-dump-dir writes the searched (whitened) series and
+    template 0's resampled series and power spectrum, one "%e" value per line
+    (reference dumpFloatBufferToTextFile, erp_utilities.cpp:216-233)."""
+    import numpy as np
+
+    dump = tmp_path / "dump"
+    dump.mkdir()
+    r = _run(app, _args(small, tmp_path / "r.cand", tmp_path / "c.cpt", ["-z", "--mi355x-dump-dir", str(dump)]),
+             tmp_path)
+    assert r.returncode == 0, r.stderr[-2000:]
+    series = np.loadtxt(dump / "dump_series.txt")
+    x = np.loadtxt(dump / "dump_resampled_t0.txt")
+    ps = np.loadtxt(dump / "dump_power_t0.txt")
+    assert len(x) == 2 * (len(ps) - 1) or len(x) == 2 * len(ps) - 1
+    assert len(series) <= len(x)
+    # the dumped spectrum is the normalised power of the dumped resampled series
+    ref = np.abs(np.fft.rfft(x.astype(np.float64))) ** 2 / len(x)
+    ref[0] = 0.0
+    scale = ref[1:].mean()
+    assert np.max(np.abs(ps - ref[:len(ps)]) / np.maximum(ref[:len(ps)], scale)) < 1e-3
+    first = (dump / "dump_power_t0.txt").read_text().splitlines()[1]
+    assert "e" in first  # "%e" format

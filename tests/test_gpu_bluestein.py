@@ -1,0 +1,104 @@
+"""Every padding the reference accepts on the GPU (pytest -m gpu).
+
+The reference takes any -P in [1, 10] and FFTs nsamples = (int)(P*N_u + 0.5)
+samples (demod_binary.c:226-244, 782; cuFFT/FFTW plan any length). Lengths the
+three-pass FFT does not factor (odd N, or N/2 with a prime factor above 5) run
+as a chirp-z transform on the device (csrc/hip/bluestein.hip); these tests pin
+it against the double-precision CPU model (whose FFT is itself a chirp-z
+convolution for such lengths, checked against numpy in
+tests/test_numerics.py)."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from boinc_app_eah_brp_amd.models import BRPSearch, SearchConfig
+from boinc_app_eah_brp_amd.models.search import app_binary
+from boinc_app_eah_brp_amd.utils import synth
+
+pytestmark = pytest.mark.gpu
+
+INJ = synth.Injection(f0=97.0, P_orb=700.0, tau=0.02, psi0=0.3, amplitude=2.0)
+
+
+def _geom(brp, tmp_path, n, padding, window=100, f0=150.0):
+    x = synth.make_series(n, 65.476, INJ)
+    wu = synth.write_wu(tmp_path / "a.bin4", x)
+    hdr, series, _ = brp.read_work_unit(str(wu))
+    geom = brp.derive_geometry(hdr, dict(f0=f0, padding=padding, fA=0.08, window=window))
+    return hdr, series, geom
+
+
+@pytest.mark.parametrize("n,padding", [(1 << 16, 1.1), (1 << 16, 1.7), (1 << 17, 2.3), (1 << 18, 9.9),
+                                       (1 << 16, 3.01)])
+def test_power_spectrum_any_padding(brp, gpu, tmp_path, n, padding):
+    """Non-smooth and odd N: the device spectrum (chirp-z) matches the CPU
+    double-precision spectrum, with n_steps and the mean padding exact."""
+    _, series, geom = _geom(brp, tmp_path, n, padding)
+    N = geom["nsamples"]
+    assert brp.fft_plan(N // 2) is None or N % 2, (N, "expected a length outside the three-pass set")
+    eng = brp.HipEngine()
+    eng.init(0, 2)
+    eng.setup(geom, series, float(np.mean(series)))
+    for P, tau, psi in ((700.0, 0.02, 0.3), (1500.0, 0.3, 4.0)):
+        ps_g, ns_g = eng.power_spectrum(P, tau, psi)
+        xr, ns_c, _ = brp.cpu_resample(series, geom, P, tau, psi)
+        ps_c = brp.cpu_power_spectrum(xr, geom["fft_size"])
+        assert ns_g == ns_c
+        scale = float(np.mean(ps_c[1:]))
+        err = np.abs(ps_g.astype(np.float64) - ps_c)[1:] / np.maximum(ps_c[1:], scale)
+        assert err.max() < 2e-4, (N, padding, err.max(), int(np.argmax(err)) + 1)
+
+
+@pytest.mark.parametrize("padding", [1.1, 1.7])
+def test_whitening_any_padding(brp, gpu, tmp_path, padding):
+    """Device whitening (forward chirp-z, running median, zapping, inverse
+    chirp-z; odd N via the Hermitian extension) matches the CPU whitening."""
+    case = synth.synthetic_case(tmp_path, n=1 << 16, n_templates=1)
+    hdr, series, _ = brp.read_work_unit(case["wu"])
+    opt = dict(f0=200.0, padding=padding, fA=0.08, window=200, white=True)
+    geom = brp.derive_geometry(hdr, opt)
+    zaps = brp.read_zaplist(case["zap"])
+    w_cpu = brp.cpu_whiten(series, geom, opt, zaps)
+    eng = brp.HipEngine()
+    eng.init(0, 2)
+    eng.setup(geom, series, 0.0)
+    w_gpu = eng.whiten(opt, zaps, series)
+    rms = float(np.sqrt(np.mean(w_cpu.astype(np.float64) ** 2)))
+    assert rms > 0
+    assert np.max(np.abs(w_gpu - w_cpu)) / rms < 1e-4, (padding, geom["nsamples"])
+
+
+@pytest.mark.parametrize("padding", [1.7, 2.3])
+def test_search_any_padding_matches_cpu(brp, gpu, tmp_path, padding):
+    """Whole searches at paddings outside the three-pass set: GPU candidate
+    table equals the CPU golden model's (same bins, powers within float-FFT
+    tolerance)."""
+    from test_gpu_search import _compare_tables
+
+    inj = synth.Injection(f0=211.0, P_orb=900.0, tau=0.03, psi0=0.7, amplitude=3.0)
+    case = synth.synthetic_case(tmp_path / "c", n=1 << 16, n_templates=12, inj=inj)
+    cfg = dict(inputfile=case["wu"], templatebank=case["bank"], zaplistfile=case["zap"], f0=400.0, padding=padding,
+               fA=0.08, window=100, white=True, batch=2)
+    g = BRPSearch(SearchConfig(outputfile=str(tmp_path / "g.cand"), **cfg)).run(use_checkpoint=False)
+    c = BRPSearch(SearchConfig(outputfile=str(tmp_path / "c.cand"), use_cpu=True, **cfg), gpus=8).run(
+        use_checkpoint=False)
+    assert g.templates_run == c.templates_run == 13
+    _compare_tables(g.table, c.table)
+
+
+def test_app_any_padding_runs_on_gpu(brp, gpu, tmp_path):
+    """The BOINC application at -P 1.7 stays on the HIP backend (no CPU
+    fallback) and writes a complete result file."""
+    inj = synth.Injection(f0=211.0, P_orb=900.0, tau=0.03, psi0=0.7, amplitude=3.0)
+    case = synth.synthetic_case(tmp_path / "c", n=1 << 16, n_templates=6, inj=inj)
+    args = [str(app_binary()), "-i", case["wu"], "-t", case["bank"], "-l", case["zap"], "-o",
+            str(tmp_path / "r.cand"), "-c", str(tmp_path / "cp.cpt"), "-A", "0.08", "-P", "1.7", "-f", "400.0",
+            "-W", "-B", "100"]
+    r = subprocess.run(args, cwd=tmp_path, env=dict(os.environ, BRP_NO_RESULT_HEADER="1"), capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "chirp-z transform" in r.stderr and "CPU backend" not in r.stderr
+    lines, done = brp.read_results(str(tmp_path / "r.cand"))
+    assert done and lines

@@ -96,3 +96,28 @@ def test_batched_passes_quit_and_resume(gpu, task, sequential, tmp_path):
     for k in range(3):
         assert _body(outs[k]) == sequential[k], k
     assert not list(tmp_path.glob("cp.cpt*"))
+
+
+def test_batched_passes_resume_from_legacy_checkpoint(gpu, task, sequential, tmp_path):
+    """A reference-style checkpoint (one file, the first pass interrupted by the
+    sequential wrapper) resumes that WU at its template while the other WUs
+    start at 0; with 4-template batches the deal blocks are then no multiple
+    of the batch, and batches are cut at block boundaries. Results equal the
+    uninterrupted sequential passes byte for byte."""
+    outs = [tmp_path / f"o{k}.cand" for k in range(3)]
+    r = _run(_args(task, outs, ["--mi355x-sequential-passes"]), tmp_path, BRP_FAULT="kill_after_template:5")
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "quit prematurely" in r.stderr
+    data = (tmp_path / "cp.cpt").read_bytes()
+    n0 = struct.unpack("<I", data[:4])[0]
+    assert 5 <= n0 < 22, n0
+    env = dict(BRP_MULTI_BLOCK="1")
+    # interrupted once more inside the batched pass, then finished
+    r = _run(_args(task, outs, ["--mi355x-batch", "4"]), tmp_path, BRP_FAULT="kill_after_template:12", **env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "Continuing work on" in r.stderr
+    r = _run(_args(task, outs, ["--mi355x-batch", "4"]), tmp_path, **env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    for k in range(3):
+        assert _body(outs[k]) == sequential[k], k
+    assert not list(tmp_path.glob("cp.cpt*"))

@@ -2,6 +2,7 @@
 (pytest -m gpu). The HIP path must be the one that runs: HipEngine raises if
 the device or the extension is missing, there is no silent fallback."""
 import os
+import re
 import subprocess
 from pathlib import Path
 
@@ -204,6 +205,21 @@ def test_fault_hip_oom_temporary_exit(brp, gpu, case, tmp_path):
     assert "Temporary exit (900 s)" in r.stderr, r.stderr[-3000:]
     assert "device memory" in r.stderr
     assert not (tmp_path / "res.cand").exists()
+
+
+def test_fault_hip_oom_later_pipeline_temporary_exit(brp, gpu, case, tmp_path):
+    """Only the allocations after the first pipeline's setup fail (a later
+    pipeline takes the whitened series device to device): still a BOINC
+    temporary exit, not a hard error."""
+    probe = _app_gpu(case, tmp_path / "probe", BRP_LOGLEVEL="4")
+    assert probe.returncode == 0, probe.stderr[-3000:]
+    m = re.search(r"HIP device allocations so far: (\d+)", probe.stdout + probe.stderr)
+    assert m, (probe.stdout + probe.stderr)[-3000:]
+    n_first = int(m.group(1))
+    r = _app_gpu(case, tmp_path / "oom", BRP_FAULT=f"hip_oom:{n_first}")
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "Temporary exit (900 s)" in r.stderr, r.stderr[-3000:]
+    assert not (tmp_path / "oom" / "res.cand").exists()
 
 
 def test_fault_pinned_fail_falls_back_to_pageable(brp, gpu, case, tmp_path):

@@ -91,8 +91,12 @@ def test_lut_sin(brp):
     np.testing.assert_array_equal(reference.lut_sin(x[::50]), got)
 
 
-@pytest.mark.parametrize("n", [16, 96, 1000, 3 * 2 ** 12, 2 * 3 * 5 * 7 * 11])
+@pytest.mark.parametrize("n", [16, 96, 1000, 3 * 2 ** 12, 2 * 3 * 5 * 7 * 11,
+                               1009, 2 * 1009, 72090, 111411, 3 * 65537])
 def test_cpu_rfft(brp, n):
+    """Double-precision golden FFT against numpy, including the lengths any
+    padding -P produces (prime factors above 64 run as a chirp-z
+    convolution, csrc/core/cpu_fft.cpp)."""
     rng = np.random.default_rng(n)
     x = rng.normal(size=n)
     X = brp.rfft(x)

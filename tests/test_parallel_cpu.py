@@ -73,8 +73,15 @@ def _cp_worker(rank, world, port, opts, out_dir, kill_after):
     try:
         ss = pdist.ShardedSearch(opts, ctx, use_cpu=True)
         table, n = ss.search(chunk=7, kill_after=kill_after)
+        # every chunk started from the merged prefix: the seeds' floors rise
+        # monotonically and equal the max over ranks (identical merged tables)
+        for a, b in zip(ss.seed_floors, ss.seed_floors[1:]):
+            assert all(y >= x for x, y in zip(a, b)), (a, b)
+        mine = pdist.table_floors(table)
+        assert pdist.max_floors_over_ranks(mine, ctx) == mine
         if rank == 0:
             np.save(os.path.join(out_dir, f"n_{kill_after}.npy"), np.array([n]))
+            np.save(os.path.join(out_dir, f"floors_{kill_after}.npy"), np.array(ss.seed_floors))
     finally:
         dist.destroy_process_group()
 
@@ -102,6 +109,7 @@ def test_gloo_chunked_checkpoint_resume_equals_single(brp, tmp_path):
         mp.start_processes(_cp_worker, args=(2, _free_port(), opts, str(tmp_path), None), nprocs=2, join=True,
                            start_method="spawn")
         assert int(np.load(tmp_path / "n_None.npy")[0]) == 30
+        assert np.load(tmp_path / "floors_None.npy")[-1].max() > 0  # later chunks prune with a real floor
         single = dict(opts, outputfile=str(tmp_path / "single.cand"), checkpointfile=str(tmp_path / "single.cpt"))
         r = brp.run_search(single, 0, 0, True, False)
         assert r["templates_run"] == 30

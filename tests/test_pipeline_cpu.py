@@ -141,3 +141,20 @@ def test_candidate_table_merge_is_exact(brp):
     for a, b in ((0, 17), (17, 18), (18, 45), (45, 60)):
         merged.merge(run(range(a, b)))
     assert bytes(seq.to_bytes()) == bytes(merged.to_bytes())
+
+
+def test_fft_path_any_length(brp):
+    """ops.fft_path: smooth lengths take the three-pass FFT, every other
+    padding the chirp-z transform over a factorable length >= 2 Mb - 1."""
+    from boinc_app_eah_brp_amd import ops
+
+    p = ops.fft_path(3 << 22)
+    assert p.kind == "three-pass" and p.dft_len == 3 << 21 and p.work_ratio == 1.0
+    for P in (1.1, 1.7, 2.3, 9.9):
+        n = int(P * (1 << 22) + 0.5)
+        q = ops.fft_path(n)
+        assert q.kind == "chirp-z"
+        assert q.dft_len == (n if n % 2 else n // 2)
+        assert 2 * q.dft_len - 1 <= q.conv_len <= 1.2 * (2 * q.dft_len)
+        L1, L2, L3 = q.factors
+        assert L1 * L2 * L3 == q.conv_len

@@ -7,7 +7,10 @@ benchmark flags (-A 0.08 -P 3.0 -f 400.0 -W). Output (tracked in git):
   data/golden/bench_wu_cpu_results.txt   result file (no comment header)
   data/golden/bench_wu_cpu_table.bin     the final 5x100 CP_cand table (24000 B)
   data/golden/bench_wu_cpu_meta.json     template range, timing
-Usage: python tools/make_golden.py [--threads 8] [--end N]
+The reference's smoke target (debian/patches/benchmark.patch: first 200
+templates at -A 0.04 -P 3.0 -W -z, default -f 250) has its own golden files:
+  python tools/make_golden.py --end 200 --fA 0.04 --f0 250   (suffix _first200_A0.04_f250)
+Usage: python tools/make_golden.py [--threads 8] [--end N] [--fA 0.08] [--f0 400]
 """
 from __future__ import annotations
 
@@ -26,6 +29,8 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--threads", type=int, default=8)
     ap.add_argument("--end", type=int, default=0, help="templates [0, end) (0: whole bank)")
+    ap.add_argument("--fA", type=float, default=0.08, help="false-alarm rate -A")
+    ap.add_argument("--f0", type=float, default=400.0, help="maximum signal frequency -f")
     ap.add_argument("--out", default=str(ROOT / "data" / "golden"))
     a = ap.parse_args()
     os.environ["BRP_NO_RESULT_HEADER"] = "1"
@@ -36,17 +41,20 @@ def main() -> None:
     D = ROOT / "data" / "testwu"
     out = Path(a.out)
     out.mkdir(parents=True, exist_ok=True)
-    suffix = "" if a.end == 0 else f"_first{a.end}"
+    suffix = (("" if a.end == 0 else f"_first{a.end}") + ("" if a.fA == 0.08 else f"_A{a.fA:g}") +
+              ("" if a.f0 == 400.0 else f"_f{a.f0:g}"))
     cfg = SearchConfig.benchmark(str(D / "p2030.20151015.G187.41-00.88.N.b2s0g0.00000_1099.bin4"),
                                  str(D / "stochastic_full.bank"),
                                  str(D / "p2030.20151015.G187.41-00.88.N.b2s0g0.00000.zap"),
                                  outputfile=str(out / f"bench_wu_cpu_results{suffix}.txt"), batch=1, use_cpu=True)
+    cfg.fA = a.fA
+    cfg.f0 = a.f0
     t0 = time.time()
     r = brp.run_search(cfg.options(), 0, a.end, True, False, a.threads)
     dt = time.time() - t0
     (out / f"bench_wu_cpu_table{suffix}.bin").write_bytes(bytes(r["table"].to_bytes()))
     meta = dict(templates=r["templates_run"], templates_total=r["templates_total"], seconds=dt, threads=a.threads,
-                flags="-A 0.08 -P 3.0 -f 400.0 -W", backend="cpu golden (double FFT, reference float order)")
+                flags=f"-A {a.fA:g} -P 3.0 -f {a.f0:g} -W", backend="cpu golden (double FFT, reference float order)")
     (out / f"bench_wu_cpu_meta{suffix}.json").write_text(json.dumps(meta, indent=1) + "\n")
     print(json.dumps(meta))
 
