@@ -387,7 +387,10 @@ int wrapper_main(int argc, char** argv) {
     for (auto& s : args) av.push_back(const_cast<char*>(s.c_str()));
     av.push_back(nullptr);
     boinc::set_pass(static_cast<int>(pass), static_cast<int>(passes));
+    // the last pass's device state is left to process exit (BRP_FAST_EXIT=0: freed)
+    set_keep_device_state_on_return(pass + 1 == passes && boinc::fast_exit_enabled());
     result = search_main(static_cast<int>(args.size()), av.data());
+    set_keep_device_state_on_return(false);
     if (result) {
       log_message(LOG_ERROR, true, "Demodulation failed (error: %i)!\n", result);
       break;

@@ -38,6 +38,11 @@ struct SearchControl {
   std::function<void(uint32_t done, uint32_t total)> on_template;
 };
 
+// The application's last pass leaves its device state (buffers, streams) to
+// process exit instead of freeing it: the OS reclaims it faster than the
+// teardown (whole-process wall time). Off by default (library use).
+void set_keep_device_state_on_return(bool on);
+
 // Per-template hook of SearchSession::run: return false to stop after this template.
 using TemplateHook = std::function<bool(uint32_t done, const SearchInfo& info)>;
 

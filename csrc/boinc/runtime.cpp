@@ -361,6 +361,11 @@ char* graphics_make_shmem(const char* app_name, int size) {
   return static_cast<char*>(p);
 }
 
+bool fast_exit_enabled() {
+  const char* e = std::getenv("BRP_FAST_EXIT");
+  return !(e && std::strcmp(e, "0") == 0);
+}
+
 void finish(int status) {
   std::fprintf(stderr, "called boinc_finish(%d)\n", status);
   if (!g_standalone && g_shm) {
@@ -374,6 +379,10 @@ void finish(int status) {
   trace::phase("finish");
   std::fflush(nullptr);
   if (g_lock_fd >= 0) ::close(g_lock_fd);
+  // results, checkpoint removal and the finish marker are on disk: leave
+  // without the HIP runtime's and the C++ statics' teardown (the kernel driver
+  // reclaims device memory at process exit); BRP_FAST_EXIT=0 keeps exit()
+  if (fast_exit_enabled()) ::_exit(status);
   std::exit(status);
 }
 

@@ -95,6 +95,8 @@ char* graphics_make_shmem(const char* app_name, int size);
 int status_messages_sent();
 
 [[noreturn]] void finish(int status);
+// finish() leaves with _exit() after flushing (default; BRP_FAST_EXIT=0: exit())
+bool fast_exit_enabled();
 // quit / abort / lost heartbeat: leave without the finish marker
 [[noreturn]] void quit_exit(int status);
 [[noreturn]] void temporary_exit(int delay_s, const char* reason);

@@ -110,6 +110,10 @@ std::unique_ptr<Backend> make_replay_backend(int per_level, int batch);
 // 2^31 / 2).
 bool hip_backend_supports(const SearchGeometry& g);
 std::unique_ptr<Backend> make_hip_backend(int device, int batch, int* err);
+// Start the HIP runtime (device enumeration; no context is created, so the
+// blocking-sync flag can still be set): called on a helper thread while the
+// host reads the work unit, bank and zaplist.
+void hip_runtime_warm_up();
 // Host waits on HIP work sleep (hipDeviceScheduleBlockingSync) instead of
 // spinning; set before the first backend is created (the BOINC app does).
 void hip_set_blocking_sync(bool on);

@@ -16,6 +16,9 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <memory>
+#include <tuple>
+#include <mutex>
 #include <string>
 #include <unordered_map>
 
@@ -226,6 +229,66 @@ std::vector<float2> stage_table(uint32_t L) {
   return t;
 }
 
+// row passes (pass 3): the padded table, then W_L^{jm q} as [q - 1][jm] for the
+// last radix-16 stage, jm < L / 16 (fft_block.hpp, copy_row_twiddles)
+std::vector<float2> stage_table_rows(uint32_t L) {
+  std::vector<float2> t = stage_table(L);
+  for (uint32_t q = 1; q < 16; ++q)
+    for (uint32_t jm = 0; jm < L / 16; ++jm) t.push_back(root(static_cast<uint64_t>(jm) * q, L));
+  return t;
+}
+
+// Host-built twiddle tables of one plan (single rounding from long double).
+// Every pipeline of a process (and every pass of a task) uses the same plan,
+// so they are computed once: ~80 000 long-double sin/cos per plan.
+struct HostTables {
+  std::vector<float2> st1, st2, st3, p1, p2col, p2lo, p2hi, p3;
+};
+
+const HostTables& host_tables(const FFTPlan3& plan) {
+  static std::mutex mu;
+  static std::map<std::tuple<uint32_t, uint32_t, uint32_t>, std::unique_ptr<HostTables>> cache;
+  std::lock_guard<std::mutex> lk(mu);
+  auto& slot = cache[std::make_tuple(plan.L1, plan.L2, plan.L3)];
+  if (slot) return *slot;
+  auto h = std::make_unique<HostTables>();
+  const uint32_t L1 = plan.L1, L2 = plan.L2, L3 = plan.L3, M = plan.M;
+  const uint64_t L2L3 = static_cast<uint64_t>(L2) * L3;
+  h->st1 = stage_table(L1);
+  h->st2 = stage_table(L2);
+  h->st3 = stage_table_rows(L3);
+  h->p1.resize(static_cast<size_t>(L2) * L1);
+  for (uint32_t n2 = 0; n2 < L2; ++n2)
+    for (uint32_t k1 = 0; k1 < L1; ++k1)
+      h->p1[n2 * L1 + k1] = root(static_cast<uint64_t>(n2) * k1, static_cast<uint64_t>(L1) * L2);
+  h->p2col.assign(static_cast<size_t>(L1) * L3, make_float2(0, 0));
+  for (uint32_t k1 = 0; k1 < L1; ++k1)
+    for (uint32_t n3 = 0; n3 < L3; ++n3) h->p2col[k1 * L3 + n3] = root(static_cast<uint64_t>(n3) * k1, M);
+  h->p2lo.assign(256, make_float2(0, 0));
+  for (uint32_t i = 0; i < 256; ++i) h->p2lo[i] = root(i, L2L3);
+  h->p2hi.assign(512, make_float2(0, 0));
+  for (uint32_t i = 0; i < 512 && 256ull * i < L2L3; ++i) h->p2hi[i] = root(256ull * i, L2L3);
+  // pass 3: W_{4 L3}^j = hi[j >> 5] * lo[j & 31], stored as [lo 32 | hi 4 L3 / 32]
+  h->p3.assign(32 + 4ull * L3 / 32, make_float2(0, 0));
+  for (uint32_t i = 0; i < 32; ++i) h->p3[i] = root(i, 4ull * L3);
+  for (uint32_t m = 0; m < 4 * L3 / 32; ++m) h->p3[32 + m] = root(32ull * m, 4ull * L3);
+  slot = std::move(h);
+  return *slot;
+}
+
+// W_period two-level tables, cached per period like the plan tables
+const std::pair<std::vector<float2>, std::vector<float2>>& twiddles_cached(uint64_t period) {
+  static std::mutex mu;
+  static std::map<uint64_t, std::unique_ptr<std::pair<std::vector<float2>, std::vector<float2>>>> cache;
+  std::lock_guard<std::mutex> lk(mu);
+  auto& slot = cache[period];
+  if (!slot) {
+    slot = std::make_unique<std::pair<std::vector<float2>, std::vector<float2>>>();
+    build_twiddles(period, slot->first, slot->second);
+  }
+  return *slot;
+}
+
 }  // namespace
 
 struct HipEngine::Impl {
@@ -378,32 +441,12 @@ struct HipEngine::Impl {
   }
 
   int build_tables() {
-    const uint32_t L1 = plan.L1, L2 = plan.L2, L3 = plan.L3, M = plan.M;
-    const uint64_t L2L3 = static_cast<uint64_t>(L2) * L3;
-    std::vector<float2> v;
+    const HostTables& h = host_tables(plan);
     int rc;
-    if ((rc = upload(t_st1, stage_table(L1)))) return rc;
-    if ((rc = upload(t_st2, stage_table(L2)))) return rc;
-    if ((rc = upload(t_st3, stage_table(L3)))) return rc;
-    v.resize(static_cast<size_t>(L2) * L1);
-    for (uint32_t n2 = 0; n2 < L2; ++n2)
-      for (uint32_t k1 = 0; k1 < L1; ++k1) v[n2 * L1 + k1] = root(static_cast<uint64_t>(n2) * k1, static_cast<uint64_t>(L1) * L2);
-    if ((rc = upload(t_p1, v))) return rc;
-    v.assign(static_cast<size_t>(L1) * L3, make_float2(0, 0));
-    for (uint32_t k1 = 0; k1 < L1; ++k1)
-      for (uint32_t n3 = 0; n3 < L3; ++n3) v[k1 * L3 + n3] = root(static_cast<uint64_t>(n3) * k1, M);
-    if ((rc = upload(t_p2col, v))) return rc;
-    v.assign(256, make_float2(0, 0));
-    for (uint32_t i = 0; i < 256; ++i) v[i] = root(i, L2L3);
-    if ((rc = upload(t_p2lo, v))) return rc;
-    v.assign(512, make_float2(0, 0));
-    for (uint32_t i = 0; i < 512 && 256ull * i < L2L3; ++i) v[i] = root(256ull * i, L2L3);
-    if ((rc = upload(t_p2hi, v))) return rc;
-    // pass 3: W_{4 L3}^j = hi[j >> 5] * lo[j & 31], stored as [lo 32 | hi 4 L3 / 32]
-    v.assign(32 + 4ull * L3 / 32, make_float2(0, 0));
-    for (uint32_t i = 0; i < 32; ++i) v[i] = root(i, 4ull * L3);
-    for (uint32_t m = 0; m < 4 * L3 / 32; ++m) v[32 + m] = root(32ull * m, 4ull * L3);
-    if ((rc = upload(t_p3, v))) return rc;
+    if ((rc = upload(t_st1, h.st1)) || (rc = upload(t_st2, h.st2)) || (rc = upload(t_st3, h.st3)) ||
+        (rc = upload(t_p1, h.p1)) || (rc = upload(t_p2col, h.p2col)) || (rc = upload(t_p2lo, h.p2lo)) ||
+        (rc = upload(t_p2hi, h.p2hi)) || (rc = upload(t_p3, h.p3)))
+      return rc;
     return 0;
   }
 
@@ -676,6 +719,12 @@ void log_mem_status(int device, const char* when) {
 
 void hip_set_blocking_sync(bool on) { g_blocking_sync = on; }
 
+void hip_runtime_warm_up() {
+  int n = 0;
+  (void)hipGetDeviceCount(&n);
+  (void)hipGetLastError();
+}
+
 int hip_running_median(int device, const std::vector<float>& in, uint32_t W, std::vector<float>& out, int reps,
                        double* ms_per_call) {
   if (W == 0 || in.size() < W) return RADPUL_EVAL;
@@ -853,9 +902,8 @@ int HipEngine::setup_impl(const SearchGeometry& g, const float* host_series, con
   if ((rc = d.partials.alloc(B * std::max(d.plan.wg1(), d.bs_nparts)))) return rc;
   if (d.bs) {
     if ((rc = d.bs_a.alloc(B * d.plan.M)) || (rc = d.bs_h.alloc(d.plan.M))) return rc;
-    std::vector<float2> chi, clo;
-    build_twiddles(2ull * d.bs_Mb, chi, clo);
-    if ((rc = d.upload(d.bs_chirp_hi, chi)) || (rc = d.upload(d.bs_chirp_lo, clo))) return rc;
+    const auto& ch = twiddles_cached(2ull * d.bs_Mb);
+    if ((rc = d.upload(d.bs_chirp_hi, ch.first)) || (rc = d.upload(d.bs_chirp_lo, ch.second))) return rc;
   } else {
     d.bs_a.release();
     d.bs_h.release();
@@ -911,8 +959,9 @@ int HipEngine::setup_impl(const SearchGeometry& g, const float* host_series, con
   }
   d.io_next = d.io_head = 0;
   d.select_io(0);
-  std::vector<float2> hi, lo;
-  build_twiddles(2ull * g.nsamples, hi, lo);
+  const auto& twc = twiddles_cached(2ull * g.nsamples);
+  const std::vector<float2>& hi = twc.first;
+  const std::vector<float2>& lo = twc.second;
   if ((rc = d.tw_hi.alloc(hi.size()))) return rc;
   if ((rc = d.tw_lo.alloc(lo.size()))) return rc;
   BRP_HIP_CHECK(hipMemcpy(d.tw_hi.p, hi.data(), hi.size() * sizeof(float2), hipMemcpyHostToDevice),

@@ -169,12 +169,38 @@ struct BlockLayout {
   }
 };
 
+// Stage twiddle table W_L^e (e < L) stored at e + e/16 (kTwPad<L> entries) so the
+// stride-q reads of a radix-16 stage do not collide on LDS banks. The host
+// precomputes it in exactly this order; kernels copy it contiguously to LDS.
+template <int L>
+constexpr int kTwPad = L + L / 16 + 1;
+
+// 8-byte LDS load kept a ds_read_b64: left to itself the load-store optimiser
+// pairs neighbouring loads into ds_read2_b64, which the LDS services as 4 x 16
+// lanes on 32 banks -- twice the cycles of two ds_read_b64, and the row
+// layout's skews assume the 64-bank b64 mapping (cdna_hip_programming.md §2)
+__device__ __forceinline__ float2 lds_ld64(const float2* p) {
+  using f2 = float __attribute__((ext_vector_type(2)));
+  const f2 v = *(const volatile f2 __attribute__((address_space(3)))*)(p);
+  return make_float2(v.x, v.y);
+}
+
+// Row passes (pass 3): the last radix-16 stage (Ns = L / 16) reads its
+// twiddles W_L^{jm q} from a q-major block [q - 1][jm] appended to the padded
+// stage table, so the 16 butterflies of a row read 16 consecutive entries.
+// (From the padded table the stride-jm reads collided: 44 extra LDS cycles per
+// wave, all of pass 3's bank conflicts in profiles/pmc_bytes_pruned_hs_r2.txt.)
+template <int L>
+constexpr int kTwRowExtra = 15 * (L / 16);
+
 // One Stockham stage LDS -> LDS (in place, two barriers).
 template <int L, int NCOL, int TPC, bool ROWMAJOR, int R, int Ns>
 __device__ __forceinline__ void block_stage(float2* lds, const float2* tw_lds) {
   using Lay = BlockLayout<L, NCOL, TPC, ROWMAJOR>;
   constexpr int kBf = L / R;                       // butterflies per column
   constexpr int kNb = (kBf + TPC - 1) / TPC;       // butterflies per thread
+  constexpr bool kQMajor = ROWMAJOR && Ns > 1 && Ns * R == L;
+  static_assert(!kQMajor || R == 16, "row passes end in a radix-16 stage");
   int c, tj;
   Lay::coords(threadIdx.x, c, tj);
   float2 v[kNb][R];
@@ -183,13 +209,22 @@ __device__ __forceinline__ void block_stage(float2* lds, const float2* tw_lds) {
     const int j = tj + u * TPC;
     if (kBf % TPC == 0 || j < kBf) {
 #pragma unroll
-      for (int q = 0; q < R; ++q) v[u][q] = lds[Lay::idx(j + q * kBf, c)];
+      for (int q = 0; q < R; ++q) {
+        const float2* p = &lds[Lay::idx(j + q * kBf, c)];
+        v[u][q] = ROWMAJOR ? lds_ld64(p) : *p;
+      }
       if (Ns > 1) {
         const int jm = j % Ns;
 #pragma unroll
         for (int q = 1; q < R; ++q) {
-          const int e = (jm * q * (L / (Ns * R))) % L;
-          v[u][q] = cmul(v[u][q], tw_lds[e + (e >> 4)]);  // padded: stride-q reads hit distinct banks
+          float2 w;
+          if constexpr (kQMajor) {
+            w = lds_ld64(&tw_lds[kTwPad<L> + (q - 1) * Ns + jm]);
+          } else {
+            const int e = (jm * q * (L / (Ns * R))) % L;
+            w = tw_lds[e + (e >> 4)];  // padded: stride-q reads hit distinct banks
+          }
+          v[u][q] = cmul(v[u][q], w);
         }
       }
       Dft<R>::run(v[u]);
@@ -364,15 +399,17 @@ __device__ __forceinline__ float2 rot_mi(float2 a, uint32_t q) {
   }
 }
 
-// Stage twiddle table W_L^e (e < L) stored at e + e/16 (kTwPad<L> entries) so the
-// stride-q reads of a radix-16 stage do not collide on LDS banks. The host
-// precomputes it in exactly this order; kernels copy it contiguously to LDS.
-template <int L>
-constexpr int kTwPad = L + L / 16 + 1;
 
 template <int L>
 __device__ __forceinline__ void copy_stage_twiddles(float2* tw_lds, const float2* __restrict__ st) {
   for (int e = threadIdx.x; e < kTwPad<L>; e += blockDim.x) tw_lds[e] = st[e];
+}
+
+// row-pass stage table: padded W_L^e, then the last stage's q-major block
+// (host: stage_table_rows in hip_engine.cpp)
+template <int L>
+__device__ __forceinline__ void copy_row_twiddles(float2* tw_lds, const float2* __restrict__ st) {
+  for (int e = threadIdx.x; e < kTwPad<L> + kTwRowExtra<L>; e += blockDim.x) tw_lds[e] = st[e];
 }
 
 }  // namespace hipk

@@ -234,7 +234,7 @@ __global__ void __launch_bounds__(kNcol * 16) pass1_pruned3_kernel(Pass1Args a) 
   if (tj < NB3) {
     float2 z[16];
 #pragma unroll
-    for (int q = 0; q < 16; ++q) z[q] = data[(tj + NB3 * q) * kNcol + c];
+    for (int q = 0; q < 16; ++q) z[q] = lds_ld64(&data[(tj + NB3 * q) * kNcol + c]);  // b64, not read2
 #pragma unroll
     for (int q = 1; q < 16; ++q) z[q] = cmul(z[q], wl[tj * q]);
     Dft<16>::run(z);
@@ -242,7 +242,7 @@ __global__ void __launch_bounds__(kNcol * 16) pass1_pruned3_kernel(Pass1Args a) 
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int k1 = tj + NB3 * q;
-      out[static_cast<size_t>(k1) * a.L2L3] = cmul(z[q], two[k1]);
+      out[static_cast<size_t>(k1) * a.L2L3] = cmul(z[q], lds_ld64(&two[k1]));
     }
   }
   const double tot = block_sum<NT>(static_cast<double>(fsum), red);
@@ -539,10 +539,10 @@ __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Arg
   // data | stage twiddles W_L | W_{4L} (= W_2N^{C i}) as lo[32] | hi[4L/32]
   constexpr int kT4 = 32 + L4 / 32;
   static_assert(L4 % 32 == 0, "two-level W_{4L} table");
-  __shared__ __attribute__((aligned(16))) float2 smem[Lay::kLds + kTwPad<L> + kT4];
+  __shared__ __attribute__((aligned(16))) float2 smem[Lay::kLds + kTwPad<L> + kTwRowExtra<L> + kT4];
   float2* data = smem;
   float2* twl = smem + Lay::kLds;
-  float2* t4 = twl + kTwPad<L>;
+  float2* t4 = twl + kTwPad<L> + kTwRowExtra<L>;
   // W_{4L}^j, j < 4L
   auto w4 = [&](uint32_t j) { return cmul(t4[32 + (j >> 5)], t4[j & 31u]); };
 
@@ -592,7 +592,7 @@ __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Arg
       for (int q = 0; q < R0; ++q) data[Lay::idx(R0 * j + q, slot)] = v[u][q];
     }
   }
-  copy_stage_twiddles<L>(twl, a.tb.st3);
+  copy_row_twiddles<L>(twl, a.tb.st3);
   {
     for (int i = threadIdx.x; i < kT4; i += NT) t4[i] = a.tb.p3[i];
   }
@@ -664,7 +664,7 @@ __global__ void __launch_bounds__(ROWS * tpc_for<L>()) pass3_plain_kernel(Pass3P
   constexpr int TPC = tpc_for<L>();
   constexpr int NT = ROWS * TPC;
   using Lay = BlockLayout<L, ROWS, TPC, true>;
-  __shared__ __attribute__((aligned(16))) float2 smem[Lay::kLds + kTwPad<L>];
+  __shared__ __attribute__((aligned(16))) float2 smem[Lay::kLds + kTwPad<L> + kTwRowExtra<L>];
   float2* data = smem;
   float2* twl = smem + Lay::kLds;
   const uint32_t c0 = blockIdx.x * ROWS;
@@ -674,7 +674,7 @@ __global__ void __launch_bounds__(ROWS * tpc_for<L>()) pass3_plain_kernel(Pass3P
     const float2* src = a.buf + row_base(c0 + slot, a.L1, a.L2, a.L3);
     for (int r = tj; r < L; r += TPC) data[Lay::idx(r, slot)] = src[r];
   }
-  copy_stage_twiddles<L>(twl, a.tb.st3);
+  copy_row_twiddles<L>(twl, a.tb.st3);
   __syncthreads();
   BlockFFT<L, ROWS, TPC, true>::run(data, twl);
   // natural-order output z[c + C*k3] = conj(Z)*scale -> real samples 2n, 2n+1
@@ -699,7 +699,7 @@ __global__ void __launch_bounds__(ROWS * tpc_for<L>()) pass3_cplx_kernel(Pass3Cp
   constexpr int TPC = tpc_for<L>();
   constexpr int NT = ROWS * TPC;
   using Lay = BlockLayout<L, ROWS, TPC, true>;
-  __shared__ __attribute__((aligned(16))) float2 smem[Lay::kLds + kTwPad<L>];
+  __shared__ __attribute__((aligned(16))) float2 smem[Lay::kLds + kTwPad<L> + kTwRowExtra<L>];
   float2* data = smem;
   float2* twl = smem + Lay::kLds;
   const int b = blockIdx.y;
@@ -711,7 +711,7 @@ __global__ void __launch_bounds__(ROWS * tpc_for<L>()) pass3_cplx_kernel(Pass3Cp
     const float2* src = buf + row_base(c0 + slot, a.L1, a.L2, a.L3);
     for (int r = tj; r < L; r += TPC) data[Lay::idx(r, slot)] = src[r];
   }
-  copy_stage_twiddles<L>(twl, a.tb.st3);
+  copy_row_twiddles<L>(twl, a.tb.st3);
   __syncthreads();
   BlockFFT<L, ROWS, TPC, true>::run(data, twl);
   const int s = threadIdx.x % ROWS;
