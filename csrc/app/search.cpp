@@ -222,7 +222,11 @@ int SearchSession::open(const SearchOptions& opt, const SearchControl& ctl) {
     for (int h = 0; h < 5; ++h)
       log_message(LOG_INFO, false, "%s = %g\n", names[h], 0.5 * chisq_Qinv_even(d.g.prob, 1 << h));
   }
-  if (hip_start.joinable()) hip_start.join();
+  if (hip_start.joinable()) {
+    hip_prepare_host_tables(d.g);  // host work while the runtime starts
+    trace::phase("host FFT tables");
+    hip_start.join();
+  }
   trace::phase("HIP runtime up");
   // one backend per device; with the CPU golden model, one per worker thread
   int ngpu = std::max(1, ctl.gpus);

@@ -114,6 +114,10 @@ std::unique_ptr<Backend> make_hip_backend(int device, int batch, int* err);
 // blocking-sync flag can still be set): called on a helper thread while the
 // host reads the work unit, bank and zaplist.
 void hip_runtime_warm_up();
+// Host-side FFT twiddle tables of the geometry's plan, computed ahead (they are
+// cached per plan and shared by every pipeline); meant to overlap the HIP
+// runtime start-up.
+void hip_prepare_host_tables(const SearchGeometry& g);
 // Host waits on HIP work sleep (hipDeviceScheduleBlockingSync) instead of
 // spinning; set before the first backend is created (the BOINC app does).
 void hip_set_blocking_sync(bool on);

@@ -719,6 +719,19 @@ void log_mem_status(int device, const char* when) {
 
 void hip_set_blocking_sync(bool on) { g_blocking_sync = on; }
 
+void hip_prepare_host_tables(const SearchGeometry& g) {
+  FFTPlan3 p;
+  if (g.nsamples % 2 == 0 && make_fft_plan(g.nsamples / 2, p)) {
+    (void)host_tables(p);
+  } else {
+    const uint32_t mb = g.nsamples % 2 ? g.nsamples : g.nsamples / 2;
+    if (!make_bluestein_plan(mb, p)) return;
+    (void)host_tables(p);
+    (void)twiddles_cached(2ull * mb);
+  }
+  (void)twiddles_cached(2ull * g.nsamples);
+}
+
 void hip_runtime_warm_up() {
   int n = 0;
   (void)hipGetDeviceCount(&n);

@@ -127,7 +127,7 @@ __global__ void __launch_bounds__(kThreads) bs_power_kernel(BsPowerArgs a) {
     p = (x.x * x.x + x.y * x.y) * a.norm;
   }
   const size_t o = static_cast<size_t>(b) * a.ps_stride + k;
-  if (HALF) a.ps16[o] = static_cast<_Float16>(p);
+  if (HALF) a.ps16[o] = static_cast<_Float16>(fminf(p, 65504.0f));  // saturate: no inf in the fp16 spectrum
   else a.ps[o] = p;
 }
 

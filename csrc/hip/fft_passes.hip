@@ -502,7 +502,9 @@ struct P3Emit {
   }
   __device__ __forceinline__ void store(uint32_t k, float p) const {
     const size_t o = static_cast<size_t>(b) * a.ps_stride + k;
-    if (MODE == P3_POWER16) a.ps16[o] = static_cast<_Float16>(p);
+    // fp16 spectrum (config 5) saturates at the largest finite half: a strong
+    // line stays a (clamped) candidate instead of an inf in the sums
+    if (MODE == P3_POWER16) a.ps16[o] = static_cast<_Float16>(fminf(p, 65504.0f));
     else a.ps[o] = p;
   }
   __device__ __forceinline__ void operator()(uint32_t k, float2 x, float2 tk, float2 ta) const {
@@ -521,7 +523,7 @@ struct P3Emit {
       }
       const float pm = (x.x * x.x + x.y * x.y) * a.norm;
       const size_t o = static_cast<size_t>(b) * a.ps_stride + a.M;
-      if (MODE == P3_POWER16) a.ps16[o] = static_cast<_Float16>(pm);
+      if (MODE == P3_POWER16) a.ps16[o] = static_cast<_Float16>(fminf(pm, 65504.0f));
       else a.ps[o] = pm;
     } else {
       a.spec[a.M] = x;
