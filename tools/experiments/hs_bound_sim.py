@@ -59,14 +59,29 @@ def main():
 
     cell_cache = {w: cells(w) for w in (2, 4, 8, 16)}
 
+    def f16_up(x):
+        """x rounded up to the next fp16 value (the packed-fp16 bound phase's
+        staging; an upper bound stays an upper bound)"""
+        h = x.astype(np.float16)
+        lo = h.astype(np.float32) < x
+        h[lo] = np.nextafter(h[lo], np.float16(np.inf))
+        return h.astype(np.float32)
+
+    # fp16 bound phase: cells rounded up to fp16, and the <= 15 fp16 additions of
+    # a level-4 sum (round-to-nearest, 2^-11 each) covered by a relative margin
+    F16_MARGIN = np.float32(1.0 + 16 * 2.0 ** -11)
+    cell_cache.update({-w: f16_up(cell_cache[w]) for w in (8, 16)})
+
     def rmax(l, lo_i, hi_i, width):
         """max over the bins harmonic l reaches for indices [lo_i, hi_i] (inclusive)"""
         lo = (l * np.maximum(lo_i, 0) + 8) >> 4
         hi = (l * np.maximum(hi_i, 0) + 8) >> 4
         if width == 1:
             src, a, b = padded, lo, hi
+        elif width == -1:
+            src, a, b = f16_up(padded), lo, hi
         else:
-            sh = width.bit_length() - 1
+            sh = abs(width).bit_length() - 1
             src, a, b = cell_cache[width], lo >> sh, hi >> sh
         m = src[np.minimum(a, len(src) - 1)]
         for d in range(1, int((b - a).max()) + 1):
@@ -95,7 +110,8 @@ def main():
             u.append(s)
         return u
 
-    def flagged(u):
+    def flagged(u, margin=np.float32(1.0)):
+        u = [x * margin for x in u]
         f = np.zeros(nblk, bool)
         per = []
         for h in range(5):
@@ -122,11 +138,17 @@ def main():
         "per-level spans, 4-bin cells": (tight, lambda l: 1 if l < 4 else 4),
         "per-level spans, bins for l<8, 8-bin cells": (tight, lambda l: 1 if l < 8 else 8),
         "per-level spans, 4-bin l<8, 8-bin": (tight, lambda l: 1 if l < 4 else (4 if l < 8 else 8)),
+        "default, 16-bin cells": (l4only, lambda l: 1 if l < 4 else 16),
+        "default, fp16 bound phase (cells/bins rounded up to fp16, +16 ulp margin)":
+            (l4only, lambda l: -1 if l < 4 else -8),
+        "default, fp16 bound phase with 16-bin cells": (l4only, lambda l: -1 if l < 4 else -16),
         "per-level spans, exact bins": (tight, lambda l: 1),
         "span 20, exact bins": (span20, lambda l: 1),
     }
     for name, (sp, wf) in variants.items():
-        print(json.dumps(dict(variant=name, template=k, thr=thr.tolist(), **flagged(bounds(sp, wf)))), flush=True)
+        margin = F16_MARGIN if "fp16" in name else np.float32(1.0)
+        print(json.dumps(dict(variant=name, template=k, thr=thr.tolist(), **flagged(bounds(sp, wf), margin))),
+              flush=True)
 
 
 if __name__ == "__main__":
