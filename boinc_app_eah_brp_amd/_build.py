@@ -64,7 +64,8 @@ def git_id() -> str:
 
 def _common_flags() -> list[str]:
     return ["-O3", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-function", "-Wno-unknown-pragmas",
-            "-D__HIP_PLATFORM_AMD__", f"-I{ROCM / 'include'}", f'-DBRP_GIT_ID="{git_id()[:40]}"']
+            "-D__HIP_PLATFORM_AMD__", f"-I{ROCM / 'include'}", f'-DBRP_GIT_ID="{git_id()[:40]}"',
+            *os.environ.get("BRP_EXTRA_CFLAGS", "").split()]  # experiment builds (scripts/build_variant.sh)
 
 
 def _headers_mtime() -> float:

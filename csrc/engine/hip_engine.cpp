@@ -355,6 +355,8 @@ struct HipEngine::Impl {
   bool hs_prune = true;         // pruned harmonic sum (BRP_HS_FULL=1: every block exactly)
   int hs_cell_shift = 3;        // its bound cells: 8 bins (BRP_HS_CELL=4: 4 bins, tighter bounds but
                                 // 44 KB LDS / 125 VGPRs per workgroup: 16.4-16.7k vs 15.6-15.8k templates/s)
+  bool hs_direct = true;        // bounds read straight from global memory (BRP_HS_DIRECT=0: LDS-staged;
+                                // +2 % fp32, +3 % config 5 in one call, profiles/README.md round 3)
   DevBuf<double> partials;      // [batch][wg1]
   DevBuf<double> delta;         // [batch] mean-padding correction
   // Per-batch I/O, double-buffered so that a pipeline can keep two batches in
@@ -660,6 +662,7 @@ struct HipEngine::Impl {
         ah.cap = cap;
         ah.prune = hs_prune;
         ah.cell_shift = hs_cell_shift;
+        ah.direct = hs_direct && hs_cell_shift == 3;
         ah.pyr = pyr.p;
         ah.pyr_stride = hipk::hs_pyr_stride(ps_stride);
         return hipk::launch_harmonic_sum(ah, nb, stream);
@@ -910,6 +913,7 @@ int HipEngine::setup_impl(const SearchGeometry& g, const float* host_series, con
   if ((rc = d.ps.alloc(B * d.ps_stride))) return rc;
   d.hs_prune = std::getenv("BRP_HS_FULL") == nullptr || std::atoi(std::getenv("BRP_HS_FULL")) == 0;
   d.hs_cell_shift = (std::getenv("BRP_HS_CELL") && std::atoi(std::getenv("BRP_HS_CELL")) == 4) ? 2 : 3;
+  d.hs_direct = std::getenv("BRP_HS_DIRECT") == nullptr || std::atoi(std::getenv("BRP_HS_DIRECT")) != 0;
   if ((rc = d.pyr.alloc(B * hipk::hs_pyr_stride(d.ps_stride)))) return rc;
   d.bs_nparts = d.bs ? hipk::bs_chirp_in_blocks(d.plan.M) : 0;
   if ((rc = d.partials.alloc(B * std::max(d.plan.wg1(), d.bs_nparts)))) return rc;

@@ -152,6 +152,26 @@ __global__ void __launch_bounds__(kNcol * tpc_for<L>()) pass1_kernel(Pass1Args a
 // butterflies in registers. The tile crosses LDS once; the last stage (radix
 // 16, Ns = 3 R2) stores its natural-order rows k1 = j + 3 R2 q straight to
 // global memory with the output twiddle W_{L1 L2}^{n2 k1}.
+// Speed-of-light ablations for experiment builds (scripts/build_variant.sh,
+// wrong results): BRP_ABLATE_P1FFT / P1RES drop pass 1's butterflies / its
+// resampling arithmetic, BRP_ABLATE_P3FFT pass 3's row FFT; the memory
+// traffic of every pass is unchanged.
+#ifdef BRP_ABLATE_P1FFT
+constexpr bool kAblateP1Fft = true;
+#else
+constexpr bool kAblateP1Fft = false;
+#endif
+#ifdef BRP_ABLATE_P1RES
+constexpr bool kAblateP1Res = true;
+#else
+constexpr bool kAblateP1Res = false;
+#endif
+#ifdef BRP_ABLATE_P3FFT
+constexpr bool kAblateP3Fft = true;
+#else
+constexpr bool kAblateP3Fft = false;
+#endif
+
 template <int R2>
 __global__ void __launch_bounds__(kNcol * 16) pass1_pruned3_kernel(Pass1Args a) {
   constexpr int L = 3 * R2 * 16;
@@ -199,8 +219,12 @@ __global__ void __launch_bounds__(kNcol * 16) pass1_pruned3_kernel(Pass1Args a) 
       const uint32_t m = m0 + h;
       int i = -1;
       if (m < td.n_steps) {
-        const float dt = resamp_del_t(m, td.p, lut_s, lut_c);
-        i = min(max(fast ? resamp_nearest_f(m, dt) : resamp_nearest(m, dt), 0), last);
+        if constexpr (kAblateP1Res) {
+          i = min(static_cast<int>(m), last);
+        } else {
+          const float dt = resamp_del_t(m, td.p, lut_s, lut_c);
+          i = min(max(fast ? resamp_nearest_f(m, dt) : resamp_nearest(m, dt), 0), last);
+        }
       }
       idx[2 * q + h] = i;
     }
@@ -225,7 +249,7 @@ __global__ void __launch_bounds__(kNcol * 16) pass1_pruned3_kernel(Pass1Args a) 
     float2 y[R2];
 #pragma unroll
     for (int q = 0; q < R2; ++q) y[q] = (s == 0 || q == 0) ? x[q] : cmul(x[q], wl[(16 * s * q) % L]);
-    Dft<R2>::run(y);
+    if constexpr (!kAblateP1Fft) Dft<R2>::run(y);
 #pragma unroll
     for (int q = 0; q < R2; ++q) data[(NB3 * tj + s + 3 * q) * kNcol + c] = y[q];
   }
@@ -237,7 +261,7 @@ __global__ void __launch_bounds__(kNcol * 16) pass1_pruned3_kernel(Pass1Args a) 
     for (int q = 0; q < 16; ++q) z[q] = lds_ld64(&data[(tj + NB3 * q) * kNcol + c]);  // b64, not read2
 #pragma unroll
     for (int q = 1; q < 16; ++q) z[q] = cmul(z[q], wl[tj * q]);
-    Dft<16>::run(z);
+    if constexpr (!kAblateP1Fft) Dft<16>::run(z);
     float2* out = a.out + static_cast<size_t>(b) * M + col_base + c;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
@@ -615,7 +639,7 @@ __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Arg
   const RowTw rt = row_twiddles(a.tw, c, n_s);
   __syncthreads();
   if constexpr (kRegStage1) BlockFFT<L, NSLOT, TPC, true>::run_rest(data, twl);
-  else BlockFFT<L, NSLOT, TPC, true>::run(data, twl);
+  else if constexpr (!kAblateP3Fft) BlockFFT<L, NSLOT, TPC, true>::run(data, twl);
 
   constexpr bool kPower = (MODE == P3_POWER || MODE == P3_POWER16);
   const bool correct = kPower && n_s > 0;

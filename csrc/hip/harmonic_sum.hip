@@ -391,9 +391,54 @@ __device__ __forceinline__ void hs_pair_max(const float* buf, int32_t I0, int32_
   }
 }
 
-template <int CK, int... Q>
-__device__ __forceinline__ void hs_bounds(std::integer_sequence<int, Q...>, const float* buf, int32_t I0,
-                                          int32_t ib, float* u) {
+// The same maxima read straight from global memory, without LDS staging:
+// for every harmonic the bins (l < 4) or 8-bin cells (l >= 4) a block reaches
+// lie in the 4 consecutive entries from lo (hi - lo <= 3, checked below), so
+// one 16-byte load per harmonic and lane covers them (the loads of a wave
+// overlap: the cache serves them). No LDS is held while the loads are in
+// flight, so the pass kernels running beside this one keep their occupancy.
+template <int CK, int Q, int MODE>
+__device__ __forceinline__ void hs_direct_max(const PsT<MODE>* P, const float* C8, int32_t ib, float& m16,
+                                              float& m20) {
+  using S = HsStage<CK>;
+  constexpr int L = kHarm[Q], K = S::lvl(L);
+  constexpr bool kTail = Q < 8;
+  // largest hi - lo over all blocks for a span of N indices
+  constexpr int kD16 = ((((L * (kBlk - 1) + 15) / 16) + (1 << K) - 1) >> K);
+  constexpr int kD20 = ((((L * (kBlkSpan - 1) + 15) / 16) + (1 << K) - 1) >> K);
+  static_assert((kTail ? kD20 : kD16) <= 3, "one 4-entry load per harmonic");
+  constexpr int kIn = ((15 * L) / 16) >> K;  // entries e <= kIn lie in [lo, h16] for every block
+  const uint32_t lo = hs_cell(L, K, ib), h16 = hs_cell(L, K, ib + kBlk - 1);
+  const uint32_t h20 = kTail ? hs_cell(L, K, ib + kBlkSpan - 1) : h16;
+  float x[4];
+  if constexpr (K > 0 || MODE == HS_F32) {
+    using f4u = float __attribute__((ext_vector_type(4), aligned(4)));
+    const float* src = K > 0 ? C8 : reinterpret_cast<const float*>(P);
+    const f4u v = *reinterpret_cast<const f4u*>(src + lo);
+    x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) x[e] = static_cast<float>(P[lo + e]);
+  }
+  const float ninf = -__builtin_inff();
+  const uint32_t d16 = h16 - lo, d20 = h20 - lo;
+  float a = x[0], t = ninf;
+#pragma unroll
+  for (int e = 1; e <= (kTail ? kD20 : kD16); ++e) {
+    if (e <= kIn) {
+      a = fmaxf(a, x[e]);
+    } else {
+      if (e <= kD16) a = fmaxf(a, static_cast<uint32_t>(e) <= d16 ? x[e] : ninf);
+      if constexpr (kTail) t = fmaxf(t, static_cast<uint32_t>(e) <= d20 ? x[e] : ninf);
+    }
+  }
+  m16 = a;
+  m20 = kTail ? fmaxf(a, t) : a;
+}
+
+template <int CK, bool DIRECT, int MODE, int... Q>
+__device__ __forceinline__ void hs_bounds(std::integer_sequence<int, Q...>, const float* buf, const PsT<MODE>* P,
+                                          const float* C8, int32_t I0, int32_t ib, float* u) {
   if constexpr (CK == 3) {
     // running sums in the reference order, harmonic by harmonic; each group's
     // partial sums are pinned (empty volatile asm) before the next group's
@@ -402,7 +447,8 @@ __device__ __forceinline__ void hs_bounds(std::integer_sequence<int, Q...>, cons
     // 5 waves per SIMD)
     float m16, m20, x16, x20;
     auto hm = [&](auto qc, float& a16, float& a20) {
-      hs_pair_max<CK, decltype(qc)::value>(buf, I0, ib, a16, a20);
+      if constexpr (DIRECT) hs_direct_max<CK, decltype(qc)::value, MODE>(P, C8, ib, a16, a20);
+      else hs_pair_max<CK, decltype(qc)::value>(buf, I0, ib, a16, a20);
     };
     using std::integral_constant;
     auto pin = [](float& p, float& q) { asm volatile("" : "+v"(p), "+v"(q)); };
@@ -446,6 +492,8 @@ __device__ __forceinline__ void hs_bounds(std::integer_sequence<int, Q...>, cons
     (void)m20;
     (void)x20;
   } else {  // 4-bin cells (switch): pair strides of 2 would collide; b32 reads
+    (void)P;
+    (void)C8;
     const float m16[16] = {hs_span_max<CK, Q, kBlk>(buf, I0, ib)...};
     float m20[8];
 #pragma unroll
@@ -469,24 +517,28 @@ __device__ __forceinline__ void hs_bounds(std::integer_sequence<int, Q...>, cons
 // of harmonic_sum_kernel for the groups whose first index lies in the block.
 // (No global block list: an atomic per wave on one counter serialised a first
 // version at 39 us.)
-template <int CK, int MODE>
+template <int CK, int MODE, bool DIRECT>
 __global__ void __launch_bounds__(256) hs_pruned_kernel(HSArgs a, uint32_t nblk) {
 #pragma clang fp contract(off)
+  static_assert(!DIRECT || CK == 3, "direct bound reads: 8-bin cells");
   constexpr int kSubs = kWave / kBlkSpan;  // 3
-  __shared__ __attribute__((aligned(16))) float stage[4][HsStage<CK>::kCells];
+  __shared__ __attribute__((aligned(16))) float stage[DIRECT ? 1 : 4][DIRECT ? 4 : HsStage<CK>::kCells];
   __shared__ float sv[4][kSubs][4][kBlkSpan];
   const int b = blockIdx.y;
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
   const uint32_t wave_blk0 = blockIdx.x * 256u + static_cast<uint32_t>(wave * kWave);
   if (wave_blk0 >= nblk) return;  // whole wave
+#ifdef BRP_ABLATE_HS
+  return;  // speed-of-light ablation (experiment builds only: no candidates)
+#endif
   const uint32_t blk = wave_blk0 + lane;
   const PsT<MODE>* P = ps_row<MODE>(a, b);
   const float* thr = a.thr + static_cast<size_t>(b) * kHsThrStride;
   const int w2 = static_cast<int>(a.w2), fhi = static_cast<int>(a.fhi), hhi = static_cast<int>(a.hhi);
   const int32_t I0 = a.i_start + static_cast<int32_t>(kBlk * wave_blk0);
-  float* buf = stage[wave];
-  hs_stage_all<CK>(std::make_integer_sequence<int, 16>{}, buf, P, a.pyr + static_cast<size_t>(b) * a.pyr_stride,
-                   a.pyr_stride, a.ps_stride, I0, lane);
+  float* buf = stage[DIRECT ? 0 : wave];
+  const float* C8 = a.pyr + static_cast<size_t>(b) * a.pyr_stride;
+  if constexpr (!DIRECT) hs_stage_all<CK>(std::make_integer_sequence<int, 16>{}, buf, P, C8, a.pyr_stride, a.ps_stride, I0, lane);
   // LDS operations of one wave complete in order; keep the compiler from moving them
   auto wave_sync = [] {
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
@@ -494,11 +546,15 @@ __global__ void __launch_bounds__(256) hs_pruned_kernel(HSArgs a, uint32_t nblk)
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
   };
   wave_sync();
+#ifdef BRP_ABLATE_HS_STAGE
+  if (buf[lane] == -1.0f) a.list[1].x = 0;  // keep the staging live; never true for powers
+  return;  // ablation: staging only
+#endif
   bool flag = false;
   if (blk < nblk) {
     const int32_t ib = I0 + kBlk * lane;
     float u[5];
-    hs_bounds<CK>(std::make_integer_sequence<int, 16>{}, buf, I0, ib, u);
+    hs_bounds<CK, DIRECT, MODE>(std::make_integer_sequence<int, 16>{}, buf, P, C8, I0, ib, u);
 #pragma unroll
     for (int h = 0; h <= 4; ++h) {
       const int off = h ? 1 << (h - 1) : 0;
@@ -507,6 +563,10 @@ __global__ void __launch_bounds__(256) hs_pruned_kernel(HSArgs a, uint32_t nblk)
     }
   }
   unsigned long long mask = __ballot(flag);
+#ifdef BRP_ABLATE_HS_EXACT
+  if (mask != 0 && lane == 0 && thr[0] < 0.0f) a.list[1].x = 0;  // keep the bounds live
+  return;  // ablation: staging + bounds, no exact sums
+#endif
   if (mask == 0) return;
 
   const int sub = lane / kBlkSpan, li = lane % kBlkSpan;
@@ -587,17 +647,19 @@ hipError_t launch_harmonic_sum(const HSArgs& a, int batch, hipStream_t s) {
     const uint32_t nblk = hs_num_blocks(a.i_start, a.hhi);
     if (nblk == 0) return hipSuccess;
     const dim3 gc((hs_pyr_stride(a.ps_stride) + 255) / 256, batch), gp((nblk + 255) / 256, batch);
-#define BRP_HS_PRUNED(CK, MODE)                                              \
-  do {                                                                      \
-    hipLaunchKernelGGL((hs_cells_kernel<CK, MODE>), gc, dim3(256), 0, s, a); \
-    hipLaunchKernelGGL((hs_pruned_kernel<CK, MODE>), gp, dim3(256), 0, s, a, nblk); \
+#define BRP_HS_PRUNED(CK, MODE, DIRECT)                                              \
+  do {                                                                              \
+    hipLaunchKernelGGL((hs_cells_kernel<CK, MODE>), gc, dim3(256), 0, s, a);         \
+    hipLaunchKernelGGL((hs_pruned_kernel<CK, MODE, DIRECT>), gp, dim3(256), 0, s, a, nblk); \
   } while (0)
     if (a.mode == HS_F16) {
-      if (a.cell_shift == 2) BRP_HS_PRUNED(2, HS_F16);
-      else BRP_HS_PRUNED(3, HS_F16);
+      if (a.cell_shift == 2) BRP_HS_PRUNED(2, HS_F16, false);
+      else if (a.direct) BRP_HS_PRUNED(3, HS_F16, true);
+      else BRP_HS_PRUNED(3, HS_F16, false);
     } else {
-      if (a.cell_shift == 2) BRP_HS_PRUNED(2, HS_F32);
-      else BRP_HS_PRUNED(3, HS_F32);
+      if (a.cell_shift == 2) BRP_HS_PRUNED(2, HS_F32, false);
+      else if (a.direct) BRP_HS_PRUNED(3, HS_F32, true);
+      else BRP_HS_PRUNED(3, HS_F32, false);
     }
 #undef BRP_HS_PRUNED
     return hipGetLastError();

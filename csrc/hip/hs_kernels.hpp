@@ -33,6 +33,7 @@ struct HSArgs {
   // bins (2 or 3), [batch][pyr_stride]
   bool prune;
   int cell_shift;
+  bool direct;  // bounds read straight from global memory (no LDS staging; 8-bin cells)
   float* pyr;
   uint32_t pyr_stride;
 };

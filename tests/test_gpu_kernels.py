@@ -60,14 +60,16 @@ def test_power_spectrum_bench_size(brp, gpu):
         assert err.max() < 1e-3, (k, err.max(), int(np.argmax(err)) + 1)
 
 
-@pytest.mark.parametrize("full", ["0", "1"])
+@pytest.mark.parametrize("full,direct", [("0", "0"), ("0", "1"), ("1", "0")])
 @pytest.mark.parametrize("window", [100, 1001, 16, 10, 0])
-def test_harmonic_sum_matches_cpu_bitwise(brp, gpu, tmp_path, monkeypatch, window, full):
+def test_harmonic_sum_matches_cpu_bitwise(brp, gpu, tmp_path, monkeypatch, window, full, direct):
     """Same power spectrum in -> identical candidate bins and powers out (odd and
     small running-median windows move the first tile's start; below 16 it lies
-    before bin 0). Pruned path (bound filter + exact blocks, default) and the
-    full gather kernel (BRP_HS_FULL=1); the low thresholds flag most blocks."""
+    before bin 0). Pruned path (bound filter + exact blocks) with LDS-staged
+    and with direct bound reads (BRP_HS_DIRECT), and the full gather kernel
+    (BRP_HS_FULL=1); the low thresholds flag most blocks."""
     monkeypatch.setenv("BRP_HS_FULL", full)
+    monkeypatch.setenv("BRP_HS_DIRECT", direct)
     case = synth.synthetic_case(tmp_path, n=1 << 17, n_templates=2,
                                 inj=synth.Injection(f0=150.0, P_orb=900.0, tau=0.02, psi0=2.0, amplitude=3.0))
     hdr, series, _ = brp.read_work_unit(case["wu"])
@@ -86,20 +88,25 @@ def test_harmonic_sum_matches_cpu_bitwise(brp, gpu, tmp_path, monkeypatch, windo
         np.testing.assert_array_equal(pw_g, pw_c)
 
 
-@pytest.mark.parametrize("full,thr,cell", [("0", (9.0, 12.0, 16.0, 22.0, 33.0), "8"),
-                                           ("1", (9.0, 12.0, 16.0, 22.0, 33.0), "8"),
-                                           ("0", (11.0, 12.5, 15.5, 21.0, 31.0), "8"),
-                                           ("0", (13.0, 15.0, 18.0, 24.0, 34.5), "8"),
-                                           ("0", (11.0, 12.5, 15.5, 21.0, 31.0), "4"),
-                                           ("0", (18.139, 21.241, 26.269, 34.648, 48.958), "8")])
-def test_harmonic_sum_bench_size_matches_cpu_bitwise(brp, gpu, monkeypatch, full, thr, cell):
+@pytest.mark.parametrize("full,thr,cell,direct", [("0", (9.0, 12.0, 16.0, 22.0, 33.0), "8", "0"),
+                                                  ("0", (9.0, 12.0, 16.0, 22.0, 33.0), "8", "1"),
+                                                  ("1", (9.0, 12.0, 16.0, 22.0, 33.0), "8", "0"),
+                                                  ("0", (11.0, 12.5, 15.5, 21.0, 31.0), "8", "0"),
+                                                  ("0", (11.0, 12.5, 15.5, 21.0, 31.0), "8", "1"),
+                                                  ("0", (13.0, 15.0, 18.0, 24.0, 34.5), "8", "0"),
+                                                  ("0", (13.0, 15.0, 18.0, 24.0, 34.5), "8", "1"),
+                                                  ("0", (11.0, 12.5, 15.5, 21.0, 31.0), "4", "0"),
+                                                  ("0", (18.139, 21.241, 26.269, 34.648, 48.958), "8", "0"),
+                                                  ("0", (18.139, 21.241, 26.269, 34.648, 48.958), "8", "1")])
+def test_harmonic_sum_bench_size_matches_cpu_bitwise(brp, gpu, monkeypatch, full, thr, cell, direct):
     """Benchmark geometry (hhi = 5.27 M bins, two templates of a batch): the
     harmonic-sum candidates equal the CPU model's on the same spectrum, for the
     pruned path at thresholds that flag many / some / few blocks (down to the
-    search's chi^2 levels), with 8-bin (default) and 4-bin bound cells, and for
-    the full gather kernel."""
+    search's chi^2 levels), with 8-bin and 4-bin bound cells, LDS-staged and
+    direct bound reads (BRP_HS_DIRECT), and for the full gather kernel."""
     monkeypatch.setenv("BRP_HS_FULL", full)
     monkeypatch.setenv("BRP_HS_CELL", cell)
+    monkeypatch.setenv("BRP_HS_DIRECT", direct)
     hdr, series, _ = brp.read_work_unit(str(WU))
     opt = dict(OPT_BENCH, white=True)
     geom = brp.derive_geometry(hdr, opt)
@@ -129,8 +136,9 @@ def test_harmonic_sum_fp16_pruned_equals_full(brp, gpu, monkeypatch, thr):
     geom = brp.derive_geometry(hdr, opt)
     P, tau, psi = brp.read_template_bank(str(BANK))
     outs = {}
-    for full in ("0", "1"):
-        monkeypatch.setenv("BRP_HS_FULL", full)
+    for full, direct in (("0", "0"), ("1", "0"), ("d", "1")):
+        monkeypatch.setenv("BRP_HS_FULL", "1" if full == "1" else "0")
+        monkeypatch.setenv("BRP_HS_DIRECT", direct)
         eng = _engine(brp, geom, series, batch=2)
         eng.set_ps_fp16(True)
         eng.whiten(opt, brp.read_zaplist(str(ZAP)), series)
@@ -139,8 +147,9 @@ def test_harmonic_sum_fp16_pruned_equals_full(brp, gpu, monkeypatch, thr):
     assert sum(len(outs["1"][k][h][0]) for k in range(2) for h in range(5)) > 0 or thr[0] > 18.0
     for k in range(2):
         for h in range(5):
-            np.testing.assert_array_equal(outs["0"][k][h][0], outs["1"][k][h][0])
-            np.testing.assert_array_equal(outs["0"][k][h][1], outs["1"][k][h][1])
+            for v in ("0", "d"):  # LDS-staged and direct bound reads
+                np.testing.assert_array_equal(outs[v][k][h][0], outs["1"][k][h][0])
+                np.testing.assert_array_equal(outs[v][k][h][1], outs["1"][k][h][1])
 
 
 def test_engine_batches_in_flight_match_process(brp, gpu):
