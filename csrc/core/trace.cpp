@@ -79,7 +79,11 @@ void phase(const char* name) {
   static double prev = 0.0;
   std::lock_guard<std::mutex> lk(mu);
   const double t = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - g_t0).count();
-  std::fprintf(stderr, "[phase] %-28s t=%8.1f ms  +%7.1f ms\n", name, t, t - prev);
+  // wall-clock stamp too, so a caller timing the whole process can split off
+  // what lies before static initialisation and after the last phase (exit)
+  const double epoch_ms =
+      std::chrono::duration<double, std::milli>(std::chrono::system_clock::now().time_since_epoch()).count();
+  std::fprintf(stderr, "[phase] %-28s t=%8.1f ms  +%7.1f ms  epoch_ms=%.3f\n", name, t, t - prev, epoch_ms);
   prev = t;
 }
 

@@ -178,11 +178,20 @@ struct PinnedBuf {
   ~PinnedBuf() { release(); }
 };
 
+// Synchronous copy on the engine's own stream. A plain hipMemcpy goes through
+// the null stream, whose first use creates one more hardware queue: 7.5-8.3 ms
+// of start-up on MI355X (tools/experiments/startup/, profiles/README.md round 3).
+hipError_t copy_sync(void* dst, const void* src, size_t bytes, hipMemcpyKind kind, hipStream_t s) {
+  const hipError_t e = hipMemcpyAsync(dst, src, bytes, kind, s);
+  if (e != hipSuccess) return e;
+  return hipStreamSynchronize(s);
+}
+
 // A fine-grained device allocation the host may read and write in place: on
 // a large-BAR device (all MI355X platforms) ROCm maps device memory into the
 // host address space at the same address. Checked with a host-written pattern
 // read back through a device copy.
-void* host_view(int device, void* p, size_t bytes) {
+void* host_view(int device, void* p, size_t bytes, hipStream_t s) {
   int large_bar = 0;
   if (hipDeviceGetAttribute(&large_bar, hipDeviceAttributeIsLargeBar, device) != hipSuccess) return nullptr;
   hipPointerAttribute_t at{};
@@ -195,7 +204,7 @@ void* host_view(int device, void* p, size_t bytes) {
   for (size_t i = 0; i < bytes; ++i) pat[i] = static_cast<uint8_t>(i * 37u + 11u);
   std::memcpy(h, pat.data(), bytes);
   std::atomic_thread_fence(std::memory_order_seq_cst);
-  if (hipMemcpy(back.data(), p, bytes, hipMemcpyDeviceToHost) != hipSuccess) return nullptr;
+  if (copy_sync(back.data(), p, bytes, hipMemcpyDeviceToHost, s) != hipSuccess) return nullptr;
   return pat == back ? h : nullptr;
 }
 
@@ -437,7 +446,7 @@ struct HipEngine::Impl {
   int upload(DevBuf<float2>& d, const std::vector<float2>& h) {
     int rc = d.alloc(h.size());
     if (rc) return rc;
-    if (hipMemcpy(d.p, h.data(), h.size() * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess)
+    if (copy_sync(d.p, h.data(), h.size() * sizeof(float2), hipMemcpyHostToDevice, stream) != hipSuccess)
       return RADPUL_HIP_MEM_COPY_HOST_DEVICE;
     return 0;
   }
@@ -851,12 +860,14 @@ int HipEngine::upload_series0(const float* host, const float* dev_src, int src_d
   if (dev_src != nullptr) {
     // device to device: same device, or a peer over xGMI (no host round trip)
     trace::Range up("brp:series_peer_copy");
-    BRP_HIP_CHECK(hipMemcpyPeer(d.series.p, d.device, dev_src, src_device, bytes), RADPUL_HIP_MEM_COPY_HOST_DEVICE);
+    BRP_HIP_CHECK(hipMemcpyPeerAsync(d.series.p, d.device, dev_src, src_device, bytes, d.stream),
+                  RADPUL_HIP_MEM_COPY_HOST_DEVICE);
+    BRP_HIP_CHECK(hipStreamSynchronize(d.stream), RADPUL_HIP_MEM_COPY_HOST_DEVICE);
     d.st.peer_series_copies += 1;
     return 0;
   }
   trace::Range up("brp:series_upload");
-  BRP_HIP_CHECK(hipMemcpy(d.series.p, host, bytes, hipMemcpyHostToDevice), RADPUL_HIP_MEM_COPY_HOST_DEVICE);
+  BRP_HIP_CHECK(copy_sync(d.series.p, host, bytes, hipMemcpyHostToDevice, d.stream), RADPUL_HIP_MEM_COPY_HOST_DEVICE);
   return 0;
 }
 
@@ -945,7 +956,7 @@ int HipEngine::setup_impl(const SearchGeometry& g, const float* host_series, con
     Impl::BatchIO& o = d.io[i];
     o.pending = false;
     if ((rc = o.in.alloc(in_bytes, d.fg_in))) return rc;
-    uint8_t* in_host = d.fg_in ? static_cast<uint8_t*>(host_view(d.device, o.in.p, in_bytes)) : nullptr;
+    uint8_t* in_host = d.fg_in ? static_cast<uint8_t*>(host_view(d.device, o.in.p, in_bytes, d.stream)) : nullptr;
     if (d.fg_in && in_host == nullptr) {
       log_message(LOG_WARN, true, "Fine-grained device memory is not host visible; copying the batch parameters.\n");
       d.fg_in = false;
@@ -960,7 +971,7 @@ int HipEngine::setup_impl(const SearchGeometry& g, const float* host_series, con
       o.h_in_p = o.h_in.p;
     }
     uint2* cands_host =
-        d.fg_out ? static_cast<uint2*>(host_view(d.device, o.cands.p, sizeof(uint2) * (1 + d.kcopy))) : nullptr;
+        d.fg_out ? static_cast<uint2*>(host_view(d.device, o.cands.p, sizeof(uint2) * (1 + d.kcopy), d.stream)) : nullptr;
     if (d.fg_out && cands_host == nullptr) {
       log_message(LOG_WARN, true, "Fine-grained device memory is not host visible; copying the results.\n");
       d.fg_out = false;
@@ -981,9 +992,9 @@ int HipEngine::setup_impl(const SearchGeometry& g, const float* host_series, con
   const std::vector<float2>& lo = twc.second;
   if ((rc = d.tw_hi.alloc(hi.size()))) return rc;
   if ((rc = d.tw_lo.alloc(lo.size()))) return rc;
-  BRP_HIP_CHECK(hipMemcpy(d.tw_hi.p, hi.data(), hi.size() * sizeof(float2), hipMemcpyHostToDevice),
+  BRP_HIP_CHECK(copy_sync(d.tw_hi.p, hi.data(), hi.size() * sizeof(float2), hipMemcpyHostToDevice, d.stream),
                 RADPUL_HIP_MEM_COPY_HOST_DEVICE);
-  BRP_HIP_CHECK(hipMemcpy(d.tw_lo.p, lo.data(), lo.size() * sizeof(float2), hipMemcpyHostToDevice),
+  BRP_HIP_CHECK(copy_sync(d.tw_lo.p, lo.data(), lo.size() * sizeof(float2), hipMemcpyHostToDevice, d.stream),
                 RADPUL_HIP_MEM_COPY_HOST_DEVICE);
   if ((rc = d.build_tables())) return rc;
   if (d.bs) {
@@ -1023,7 +1034,7 @@ int HipEngine::adopt_series(const HipEngine& src) {
     d.adopted_token.reset();
   }
   if (!share)
-    BRP_HIP_CHECK(hipMemcpy(d.series.p, s.series.p, d.g.n_unpadded * sizeof(float), hipMemcpyDeviceToDevice),
+    BRP_HIP_CHECK(copy_sync(d.series.p, s.series.p, d.g.n_unpadded * sizeof(float), hipMemcpyDeviceToDevice, d.stream),
                   RADPUL_HIP_MEM_COPY_HOST_DEVICE);
   return 0;
 }
@@ -1057,8 +1068,8 @@ int HipEngine::load_slot(uint32_t k, const std::vector<float>& series, float mu0
   BRP_HIP_CHECK(hipSetDevice(d.device), RADPUL_HIP_DEVICE_SET);
   d.own_series();
   d.mu0s[k] = mu0;
-  BRP_HIP_CHECK(hipMemcpy(d.series.p + static_cast<size_t>(k) * d.g.n_unpadded, series.data(),
-                          d.g.n_unpadded * sizeof(float), hipMemcpyHostToDevice),
+  BRP_HIP_CHECK(copy_sync(d.series.p + static_cast<size_t>(k) * d.g.n_unpadded, series.data(),
+                          d.g.n_unpadded * sizeof(float), hipMemcpyHostToDevice, d.stream),
                 RADPUL_HIP_MEM_COPY_HOST_DEVICE);
   return 0;
 }
@@ -1472,7 +1483,7 @@ int HipEngine::download_series(std::vector<float>& series) {
   BRP_HIP_CHECK(hipSetDevice(d.device), RADPUL_HIP_DEVICE_SET);
   BRP_HIP_CHECK(hipStreamSynchronize(d.stream), RADPUL_HIP_KERNEL_INVOKE);
   series.resize(d.g.n_unpadded);
-  BRP_HIP_CHECK(hipMemcpy(series.data(), d.series_in(), d.g.n_unpadded * sizeof(float), hipMemcpyDeviceToHost),
+  BRP_HIP_CHECK(copy_sync(series.data(), d.series_in(), d.g.n_unpadded * sizeof(float), hipMemcpyDeviceToHost, d.stream),
                 RADPUL_HIP_MEM_COPY_DEVICE_HOST);
   return 0;
 }

@@ -25,3 +25,14 @@ t0, t1, n = float(sys.argv[1]), float(sys.argv[2]), int(sys.argv[3])
 print(f"bench_single: {n} templates in {t1 - t0:.3f} s wall (process incl. start-up, WU read, whitening): {n / (t1 - t0):.1f} templates/s")
 PY
 grep "Throughput" app.log || true
+if grep -q "epoch_ms=" app.log; then  # BRP_PHASES=1: process start-up and exit around the phases
+  python3 - "$t0" "$t1" app.log <<'PY'
+import re, sys
+t0, t1 = float(sys.argv[1]) * 1e3, float(sys.argv[2]) * 1e3
+ph = [(m.group(1).strip(), float(m.group(2)), float(m.group(3))) for m in
+      re.finditer(r"\[phase\] (.*?) t=\s*([\d.]+) ms .*epoch_ms=([\d.]+)", open(sys.argv[3]).read())]
+first_t, first_e = ph[0][1], ph[0][2]
+static_init = first_e - first_t  # wall time of the phase clock's zero (static initialisation)
+print(f"process: exec + loading to static init {static_init - t0:.1f} ms; last phase '{ph[-1][0]}' to exit {t1 - ph[-1][2]:.1f} ms")
+PY
+fi
