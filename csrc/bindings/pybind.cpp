@@ -476,6 +476,12 @@ PYBIND11_MODULE(_brp, m) {
              check(e.power_spectrum(TemplateInput{P, tau, psi}, ps, &n_steps), "HipEngine.power_spectrum");
              return py::make_tuple(py::array_t<float>(ps.size(), ps.data()), n_steps);
            })
+      .def("bound_cells",
+           [](HipEngine& e, int k) {
+             std::vector<float> c;
+             check(e.bound_cells(k, c), "HipEngine.bound_cells");
+             return py::array_t<float>(c.size(), c.data());
+           })
       .def("benchmark_stages",
            [](HipEngine& e, py::array_t<float> P, py::array_t<float> tau, py::array_t<float> psi, int reps) {
              auto t = arrays_to_templates(P, tau, psi);

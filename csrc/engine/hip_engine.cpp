@@ -1541,6 +1541,18 @@ int HipEngine::benchmark_stages(const TemplateInput* t, int n, int reps, std::ve
   return 0;
 }
 
+int HipEngine::bound_cells(int k, std::vector<float>& cells) {
+  Impl& d = *impl_;
+  if (!d.ready || k < 0 || k >= d.batch || !d.hs_prune || d.hs_cell_shift != 3) return RADPUL_EVAL;
+  BRP_HIP_CHECK(hipSetDevice(d.device), RADPUL_HIP_DEVICE_SET);
+  BRP_HIP_CHECK(hipStreamSynchronize(d.stream), RADPUL_HIP_KERNEL_INVOKE);
+  cells.resize((d.ps_stride >> 3) + 8);
+  BRP_HIP_CHECK(copy_sync(cells.data(), d.pyr.p + static_cast<size_t>(k) * hipk::hs_pyr_stride(d.ps_stride),
+                          cells.size() * sizeof(float), hipMemcpyDeviceToHost, d.stream),
+                RADPUL_HIP_MEM_COPY_DEVICE_HOST);
+  return 0;
+}
+
 BackendStats HipEngine::stats() const { return impl_->st; }
 int HipEngine::device() const { return impl_->device; }
 const FFTPlan3& HipEngine::plan() const { return impl_->plan; }

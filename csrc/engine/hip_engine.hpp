@@ -64,6 +64,9 @@ class HipEngine {
   int power_spectrum(const TemplateInput& t, std::vector<float>& ps, uint32_t* n_steps);
   // the (whitened) series of slot 0 as the templates read it
   int download_series(std::vector<float>& series);
+  // the pruned harmonic sum's 8-bin bound cells of template k of the last
+  // batch ((ps_stride >> 3) + 8 entries)
+  int bound_cells(int k, std::vector<float>& cells);
   // time each pipeline stage (prologue, pass1, pass2, pass3, harmonic, epilogue,
   // whole batch) over `reps` back-to-back launches on one batch; microseconds
   int benchmark_stages(const TemplateInput* t, int n, int reps, std::vector<double>& us_per_launch);

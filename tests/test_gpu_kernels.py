@@ -125,6 +125,44 @@ def test_harmonic_sum_bench_size_matches_cpu_bitwise(brp, gpu, monkeypatch, full
             np.testing.assert_array_equal(outs[k][h][1], ref[h][1])
 
 
+def _host_cells(ps, geom, n):
+    """8-bin maxima of the stored spectrum (bins < min(hhi, fft_size)), zero beyond"""
+    lim = min(geom["harmonic_idx_hi"], geom["fft_size"])
+    v = np.zeros(8 * n, np.float32)
+    m = min(lim, 8 * n, len(ps))
+    v[:m] = ps[:m]
+    return v.reshape(n, 8).max(axis=1)
+
+
+@pytest.mark.parametrize("case", ["bench", "small"])
+def test_bound_cells_equal_spectrum_maxima(brp, gpu, tmp_path, case):
+    """The pruned harmonic sum's 8-bin bound cells (hs_cells_kernel) equal the
+    8-bin maxima of the spectrum pass 3 stored, bit for bit, zero beyond the
+    harmonic range (the bounds' monotonicity argument needs cells >= every bin)."""
+    opt = None
+    if case == "bench":
+        hdr, series, _ = brp.read_work_unit(str(WU))
+        opt = dict(OPT_BENCH, white=True)
+        geom = brp.derive_geometry(hdr, opt)
+        P, tau, psi = brp.read_template_bank(str(BANK))
+        P, tau, psi = P[:2], tau[:2], psi[:2]
+    else:
+        c = synth.synthetic_case(tmp_path, n=1 << 17, n_templates=2,
+                                 inj=synth.Injection(f0=150.0, P_orb=900.0, tau=0.02, psi0=2.0, amplitude=3.0))
+        hdr, series, _ = brp.read_work_unit(c["wu"])
+        geom = brp.derive_geometry(hdr, dict(f0=120.0, padding=3.0, fA=0.08, window=100))
+        P, tau, psi = (np.asarray(c[key][:2]) for key in ("P", "tau", "psi"))
+    eng = _engine(brp, geom, series, batch=2)
+    if opt is not None:  # the benchmark WU is searched whitened
+        eng.whiten(opt, brp.read_zaplist(str(ZAP)), series)
+    eng.process(P.astype(np.float32), tau.astype(np.float32), psi.astype(np.float32),
+                [18.139, 21.241, 26.269, 34.648, 48.958])
+    cells = [eng.bound_cells(k) for k in range(2)]
+    for k in range(2):
+        ps, _ = eng.power_spectrum(float(np.float32(P[k])), float(np.float32(tau[k])), float(np.float32(psi[k])))
+        np.testing.assert_array_equal(cells[k], _host_cells(np.asarray(ps), geom, len(cells[k])))
+
+
 @pytest.mark.parametrize("thr", [(9.0, 12.0, 16.0, 22.0, 33.0), (18.139, 21.241, 26.269, 34.648, 48.958)])
 def test_harmonic_sum_fp16_pruned_equals_full(brp, gpu, monkeypatch, thr):
     """Config 5 (fp16 spectrum): the pruned harmonic sum (bounds from fp32 cell
