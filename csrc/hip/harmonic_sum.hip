@@ -397,43 +397,89 @@ __device__ __forceinline__ void hs_pair_max(const float* buf, int32_t I0, int32_
 // one 16-byte load per harmonic and lane covers them (the loads of a wave
 // overlap: the cache serves them). No LDS is held while the loads are in
 // flight, so the pass kernels running beside this one keep their occupancy.
-template <int CK, int Q, int MODE>
-__device__ __forceinline__ void hs_direct_max(const PsT<MODE>* P, const float* C8, int32_t ib, float& m16,
-                                              float& m20) {
-  using S = HsStage<CK>;
-  constexpr int L = kHarm[Q], K = S::lvl(L);
-  constexpr bool kTail = Q < 8;
+template <int CK, int Q>
+struct HsDirect {
+  static constexpr int L = kHarm[Q], K = HsStage<CK>::lvl(L);
+  static constexpr bool kTail = Q < 8;
   // largest hi - lo over all blocks for a span of N indices
-  constexpr int kD16 = ((((L * (kBlk - 1) + 15) / 16) + (1 << K) - 1) >> K);
-  constexpr int kD20 = ((((L * (kBlkSpan - 1) + 15) / 16) + (1 << K) - 1) >> K);
+  static constexpr int kD16 = ((((L * (kBlk - 1) + 15) / 16) + (1 << K) - 1) >> K);
+  static constexpr int kD20 = ((((L * (kBlkSpan - 1) + 15) / 16) + (1 << K) - 1) >> K);
   static_assert((kTail ? kD20 : kD16) <= 3, "one 4-entry load per harmonic");
-  constexpr int kIn = ((15 * L) / 16) >> K;  // entries e <= kIn lie in [lo, h16] for every block
-  const uint32_t lo = hs_cell(L, K, ib), h16 = hs_cell(L, K, ib + kBlk - 1);
-  const uint32_t h20 = kTail ? hs_cell(L, K, ib + kBlkSpan - 1) : h16;
-  float x[4];
-  if constexpr (K > 0 || MODE == HS_F32) {
-    using f4u = float __attribute__((ext_vector_type(4), aligned(4)));
-    const float* src = K > 0 ? C8 : reinterpret_cast<const float*>(P);
-    const f4u v = *reinterpret_cast<const f4u*>(src + lo);
-    x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
+  static constexpr int kIn = ((15 * L) / 16) >> K;  // entries e <= kIn lie in [lo, h16] for every block
+};
+
+using f4u = float __attribute__((ext_vector_type(4), aligned(4)));
+
+// the 4 entries from lo of harmonic kHarm[Q] (dword-aligned 16-byte load)
+template <int CK, int Q, int MODE>
+__device__ __forceinline__ f4u hs_direct_load(const PsT<MODE>* P, const float* C8, int32_t ib) {
+  using H = HsDirect<CK, Q>;
+  const uint32_t lo = hs_cell(H::L, H::K, ib);
+  if constexpr (H::K > 0 || MODE == HS_F32) {
+    const float* src = H::K > 0 ? C8 : reinterpret_cast<const float*>(P);
+    return *reinterpret_cast<const f4u*>(src + lo);
   } else {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) x[e] = static_cast<float>(P[lo + e]);
+    f4u v;
+    v.x = static_cast<float>(P[lo]);
+    v.y = static_cast<float>(P[lo + 1]);
+    v.z = static_cast<float>(P[lo + 2]);
+    v.w = static_cast<float>(P[lo + 3]);
+    return v;
   }
+}
+
+// maxima over the block's 16 indices (m16) and, for the first 8 harmonics,
+// its 20-index reach (m20) from the loaded entries; entries past h16 / h20
+// are masked
+template <int CK, int Q>
+__device__ __forceinline__ void hs_direct_max(f4u v, int32_t ib, float& m16, float& m20) {
+  using H = HsDirect<CK, Q>;
+  const uint32_t lo = hs_cell(H::L, H::K, ib), h16 = hs_cell(H::L, H::K, ib + kBlk - 1);
+  const uint32_t h20 = H::kTail ? hs_cell(H::L, H::K, ib + kBlkSpan - 1) : h16;
+  const float x[4] = {v.x, v.y, v.z, v.w};
   const float ninf = -__builtin_inff();
   const uint32_t d16 = h16 - lo, d20 = h20 - lo;
   float a = x[0], t = ninf;
 #pragma unroll
-  for (int e = 1; e <= (kTail ? kD20 : kD16); ++e) {
-    if (e <= kIn) {
+  for (int e = 1; e <= (H::kTail ? H::kD20 : H::kD16); ++e) {
+    if (e <= H::kIn) {
       a = fmaxf(a, x[e]);
     } else {
-      if (e <= kD16) a = fmaxf(a, static_cast<uint32_t>(e) <= d16 ? x[e] : ninf);
-      if constexpr (kTail) t = fmaxf(t, static_cast<uint32_t>(e) <= d20 ? x[e] : ninf);
+      if (e <= H::kD16) a = fmaxf(a, static_cast<uint32_t>(e) <= d16 ? x[e] : ninf);
+      if constexpr (H::kTail) t = fmaxf(t, static_cast<uint32_t>(e) <= d20 ? x[e] : ninf);
     }
   }
   m16 = a;
-  m20 = kTail ? fmaxf(a, t) : a;
+  m20 = H::kTail ? fmaxf(a, t) : a;
+}
+
+// Bounds from direct reads: all 16 loads issued before the first use (with
+// the ordering pins the staged path needs, the compiler waited for each pair
+// of loads in turn: ~8 memory latencies per wave); sums in the reference
+// order as in hs_bounds.
+template <int CK, int MODE, int... Q>
+__device__ __forceinline__ void hs_bounds_direct(std::integer_sequence<int, Q...>, const PsT<MODE>* P,
+                                                 const float* C8, int32_t ib, float* u) {
+  const f4u v[16] = {hs_direct_load<CK, Q, MODE>(P, C8, ib)...};
+  // every load in flight before the first is consumed (the scheduler otherwise
+  // splits them into two rounds around the first maxima)
+  auto issued = [](f4u x) { asm volatile("" ::"v"(x)); };
+  (issued(v[Q]), ...);
+  float m16[16], m20[16];
+  (hs_direct_max<CK, Q>(v[Q], ib, m16[Q], m20[Q]), ...);
+  u[0] = m20[0];
+  u[1] = u[0] + m20[1];
+  u[2] = u[1] + (m20[2] + m20[3]);
+  u[3] = u[2] + (((m20[4] + m20[5]) + m20[6]) + m20[7]);
+  float w0 = m16[0];
+  w0 += m16[1];
+  w0 += m16[2] + m16[3];
+  w0 += ((m16[4] + m16[5]) + m16[6]) + m16[7];
+  float w = m16[8] + m16[9];
+  w = (w + m16[10]) + m16[11];
+  w = (w + m16[12]) + m16[13];
+  w = (w + m16[14]) + m16[15];
+  u[4] = w0 + w;
 }
 
 template <int CK, bool DIRECT, int MODE, int... Q>
@@ -447,8 +493,7 @@ __device__ __forceinline__ void hs_bounds(std::integer_sequence<int, Q...>, cons
     // 5 waves per SIMD)
     float m16, m20, x16, x20;
     auto hm = [&](auto qc, float& a16, float& a20) {
-      if constexpr (DIRECT) hs_direct_max<CK, decltype(qc)::value, MODE>(P, C8, ib, a16, a20);
-      else hs_pair_max<CK, decltype(qc)::value>(buf, I0, ib, a16, a20);
+      hs_pair_max<CK, decltype(qc)::value>(buf, I0, ib, a16, a20);
     };
     using std::integral_constant;
     auto pin = [](float& p, float& q) { asm volatile("" : "+v"(p), "+v"(q)); };
@@ -551,15 +596,21 @@ __global__ void __launch_bounds__(256) hs_pruned_kernel(HSArgs a, uint32_t nblk)
   return;  // ablation: staging only
 #endif
   bool flag = false;
+  // the five thresholds up front (uniform: scalar loads), not one guarded load
+  // per level after the bounds
+  float th[5];
+#pragma unroll
+  for (int h = 0; h <= 4; ++h) th[h] = thr[h];
   if (blk < nblk) {
     const int32_t ib = I0 + kBlk * lane;
     float u[5];
-    hs_bounds<CK, DIRECT, MODE>(std::make_integer_sequence<int, 16>{}, buf, P, C8, I0, ib, u);
+    if constexpr (DIRECT) hs_bounds_direct<CK, MODE>(std::make_integer_sequence<int, 16>{}, P, C8, ib, u);
+    else hs_bounds<CK, DIRECT, MODE>(std::make_integer_sequence<int, 16>{}, buf, P, C8, I0, ib, u);
 #pragma unroll
     for (int h = 0; h <= 4; ++h) {
       const int off = h ? 1 << (h - 1) : 0;
       const int j_lo = (ib + off) >> h, j_hi = (ib + kBlk - 1 + off) >> h;  // groups whose first index is in the block
-      flag |= (j_hi >= w2 && j_lo < fhi) && !(u[h] <= thr[h]);             // NaN bounds are kept
+      flag |= (j_hi >= w2 && j_lo < fhi) && !(u[h] <= th[h]);              // NaN bounds are kept
     }
   }
   unsigned long long mask = __ballot(flag);
