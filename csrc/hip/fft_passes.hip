@@ -194,20 +194,35 @@ __global__ void __launch_bounds__(kNcol * 16) pass1_pruned3_kernel(Pass1Args a) 
   const int tj = threadIdx.x / kNcol;
   if (a.reset != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *a.reset = 0;
 
-  for (int i = threadIdx.x; i < kLutSize; i += NT) {
-    lut_s[i] = kSinLut[i];
-    lut_c[i] = kCosLut[i];
+  // the template, the sine LUT and the twiddle tables are loaded together
+  // before the first LDS write (one memory round trip instead of three ahead
+  // of the gather)
+  static_assert(kLutSize <= NT && L <= NT, "one LUT / table entry per thread");
+  const TemplateDev td = a.tmpl[b];
+  const int tid = static_cast<int>(threadIdx.x);
+  float ls = 0.0f, lc = 0.0f;
+  float2 wv = make_float2(0.0f, 0.0f), tv = wv;
+  if (tid < kLutSize) {
+    ls = kSinLut[tid];
+    lc = kCosLut[tid];
   }
-  for (int e = threadIdx.x; e < L; e += NT) {
-    wl[e] = a.tb.st1[e + (e >> 4)];
-    two[e] = a.tb.p1[n2 * L + e];
+  if (tid < L) {
+    wv = a.tb.st1[tid + (tid >> 4)];
+    tv = a.tb.p1[n2 * L + tid];
+  }
+  if (tid < kLutSize) {
+    lut_s[tid] = ls;
+    lut_c[tid] = lc;
+  }
+  if (tid < L) {
+    wl[tid] = wv;
+    two[tid] = tv;
   }
   __syncthreads();
 
   // gather rows g + 16 q (q < R2) of column c: nearest-neighbour resampling
   // with the reference's float arithmetic (three phases keep all loads in flight)
   const bool fast = a.n_unpadded <= (1u << 23);
-  const TemplateDev td = a.tmpl[b];
   const float* series = a.series + static_cast<size_t>(td.wu) * a.n_unpadded;
   const int last = static_cast<int>(a.n_unpadded) - 1;
   int idx[2 * R2];
@@ -588,16 +603,40 @@ __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Arg
   // the register first stage needs (18.2 vs 18.9 us/template), so the
   // register path is kept for reference but disabled.
   constexpr bool kRegStage1 = false && (kBf0 % TPC == 0);
+  // Every global load of the prologue is issued before the first LDS write:
+  // row segments, stage twiddles, W_{4L} table. (A copy loop that stored each
+  // twiddle before loading the next added 3 memory round trips after the rows
+  // had arrived.)
+  constexpr int kTwN = kTwPad<L> + kTwRowExtra<L>;
+  constexpr int kTwIt = (kTwN + NT - 1) / NT;
+  static_assert(kT4 <= NT, "one W_{4L} entry per thread");
+  float2 twv[kTwIt];
+  float2 t4v = make_float2(0.0f, 0.0f);
+  auto load_tables = [&] {
+#pragma unroll
+    for (int i = 0; i < kTwIt; ++i) {
+      const int e = static_cast<int>(threadIdx.x) + i * NT;
+      twv[i] = e < kTwN ? a.tb.st3[e] : make_float2(0.0f, 0.0f);
+    }
+    if (threadIdx.x < kT4) t4v = a.tb.p3[threadIdx.x];
+  };
   if constexpr (!kRegStage1) {
     int slot, tj;
     Lay::coords(threadIdx.x, slot, tj);
     const uint32_t cs = c0 + (slot % ROWS);
     const uint32_t row = (slot < ROWS) ? cs : (a.C - cs) % a.C;
     const float4* src = reinterpret_cast<const float4*>(buf + row_base(row < a.C ? row : 0, a.L1, a.L2, a.L3));
-    for (int r = tj; r < L / 2; r += TPC) {
-      const float4 v = src[r];
-      data[Lay::idx(2 * r, slot)] = make_float2(v.x, v.y);
-      data[Lay::idx(2 * r + 1, slot)] = make_float2(v.z, v.w);
+    constexpr int kRowIt = (L / 2) / TPC;
+    static_assert((L / 2) % TPC == 0, "whole row-load iterations");
+    float4 rv[kRowIt];
+#pragma unroll
+    for (int u = 0; u < kRowIt; ++u) rv[u] = src[tj + u * TPC];
+    load_tables();
+#pragma unroll
+    for (int u = 0; u < kRowIt; ++u) {
+      const int r = tj + u * TPC;
+      data[Lay::idx(2 * r, slot)] = make_float2(rv[u].x, rv[u].y);
+      data[Lay::idx(2 * r + 1, slot)] = make_float2(rv[u].z, rv[u].w);
     }
   } else {
     int slot, tj;
@@ -617,11 +656,14 @@ __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Arg
 #pragma unroll
       for (int q = 0; q < R0; ++q) data[Lay::idx(R0 * j + q, slot)] = v[u][q];
     }
+    load_tables();
   }
-  copy_row_twiddles<L>(twl, a.tb.st3);
-  {
-    for (int i = threadIdx.x; i < kT4; i += NT) t4[i] = a.tb.p3[i];
+#pragma unroll
+  for (int i = 0; i < kTwIt; ++i) {
+    const int e = static_cast<int>(threadIdx.x) + i * NT;
+    if (e < kTwN) twl[e] = twv[i];
   }
+  if (threadIdx.x < kT4) t4[threadIdx.x] = t4v;
   // mean-padding correction delta = (sum of (sample - mu0)) / n_steps (pass 2)
   double delta = 0.0;
   uint32_t n_s = 0;
