@@ -602,7 +602,11 @@ __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Arg
   // Measured on MI355X (L = 256): 16-B row loads into LDS beat the 8-B loads
   // the register first stage needs (18.2 vs 18.9 us/template), so the
   // register path is kept for reference but disabled.
+#ifdef BRP_P3_REG_STAGE1
+  constexpr bool kRegStage1 = (kBf0 % TPC == 0);
+#else
   constexpr bool kRegStage1 = false && (kBf0 % TPC == 0);
+#endif
   // Every global load of the prologue is issued before the first LDS write:
   // row segments, stage twiddles, W_{4L} table. (A copy loop that stored each
   // twiddle before loading the next added 3 memory round trips after the rows
@@ -649,6 +653,7 @@ __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Arg
     for (int u = 0; u < kBf0 / TPC; ++u)
 #pragma unroll
       for (int q = 0; q < R0; ++q) v[u][q] = src[tj + u * TPC + q * kBf0];
+    load_tables();
 #pragma unroll
     for (int u = 0; u < kBf0 / TPC; ++u) {
       Dft<R0>::run(v[u]);
@@ -656,7 +661,6 @@ __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Arg
 #pragma unroll
       for (int q = 0; q < R0; ++q) data[Lay::idx(R0 * j + q, slot)] = v[u][q];
     }
-    load_tables();
   }
 #pragma unroll
   for (int i = 0; i < kTwIt; ++i) {
