@@ -364,6 +364,7 @@ struct HipEngine::Impl {
   bool hs_prune = true;         // pruned harmonic sum (BRP_HS_FULL=1: every block exactly)
   int hs_cell_shift = 3;        // its bound cells: 8 bins (BRP_HS_CELL=4: 4 bins, tighter bounds but
                                 // 44 KB LDS / 125 VGPRs per workgroup: 16.4-16.7k vs 15.6-15.8k templates/s)
+  bool hs_xcd = false;          // pruned HS: contiguous block ranges per XCD (BRP_HS_XCD=1)
   bool hs_direct = true;        // bounds read straight from global memory (BRP_HS_DIRECT=0: LDS-staged;
                                 // +2 % fp32, +3 % config 5 in one call, profiles/README.md round 3)
   DevBuf<double> partials;      // [batch][wg1]
@@ -672,6 +673,7 @@ struct HipEngine::Impl {
         ah.prune = hs_prune;
         ah.cell_shift = hs_cell_shift;
         ah.direct = hs_direct && hs_cell_shift == 3;
+        ah.xcd = hs_xcd;
         ah.pyr = pyr.p;
         ah.pyr_stride = hipk::hs_pyr_stride(ps_stride);
         return hipk::launch_harmonic_sum(ah, nb, stream);
@@ -925,6 +927,7 @@ int HipEngine::setup_impl(const SearchGeometry& g, const float* host_series, con
   d.hs_prune = std::getenv("BRP_HS_FULL") == nullptr || std::atoi(std::getenv("BRP_HS_FULL")) == 0;
   d.hs_cell_shift = (std::getenv("BRP_HS_CELL") && std::atoi(std::getenv("BRP_HS_CELL")) == 4) ? 2 : 3;
   d.hs_direct = std::getenv("BRP_HS_DIRECT") == nullptr || std::atoi(std::getenv("BRP_HS_DIRECT")) != 0;
+  d.hs_xcd = std::getenv("BRP_HS_XCD") != nullptr && std::atoi(std::getenv("BRP_HS_XCD")) == 1;
   if ((rc = d.pyr.alloc(B * hipk::hs_pyr_stride(d.ps_stride)))) return rc;
   d.bs_nparts = d.bs ? hipk::bs_chirp_in_blocks(d.plan.M) : 0;
   if ((rc = d.partials.alloc(B * std::max(d.plan.wg1(), d.bs_nparts)))) return rc;
@@ -947,10 +950,11 @@ int HipEngine::setup_impl(const SearchGeometry& g, const float* host_series, con
   {
     const char* fg = std::getenv("BRP_FG");
     const std::string f = fg ? fg : "";
-    // measured (profiles/README.md): parameters in place +1.9%, results in
-    // place +0.8%; default "in"
+    // measured (profiles/README.md): parameters in place +1.9 %; results in
+    // place +1.0-1.6 % once the harmonic sum no longer held LDS (round 3, 5
+    // interleaved rounds); default "both"
     d.fg_in = f.empty() || f == "in" || f == "both" || f == "1";
-    d.fg_out = f == "out" || f == "both" || f == "1";
+    d.fg_out = f.empty() || f == "out" || f == "both" || f == "1";
   }
   for (int i = 0; i < Impl::kIoSlots; ++i) {
     Impl::BatchIO& o = d.io[i];

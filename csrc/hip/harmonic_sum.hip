@@ -571,7 +571,8 @@ __global__ void __launch_bounds__(256) hs_pruned_kernel(HSArgs a, uint32_t nblk)
   __shared__ float sv[4][kSubs][4][kBlkSpan];
   const int b = blockIdx.y;
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
-  const uint32_t wave_blk0 = blockIdx.x * 256u + static_cast<uint32_t>(wave * kWave);
+  const uint32_t bx = a.xcd ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+  const uint32_t wave_blk0 = bx * 256u + static_cast<uint32_t>(wave * kWave);
   if (wave_blk0 >= nblk) return;  // whole wave
 #ifdef BRP_ABLATE_HS
   return;  // speed-of-light ablation (experiment builds only: no candidates)

@@ -34,6 +34,7 @@ struct HSArgs {
   bool prune;
   int cell_shift;
   bool direct;  // bounds read straight from global memory (no LDS staging; 8-bin cells)
+  bool xcd;     // pruned kernel: contiguous block ranges per XCD (BRP_HS_XCD=1, experiment)
   float* pyr;
   uint32_t pyr_stride;
 };
