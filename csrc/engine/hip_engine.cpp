@@ -300,11 +300,23 @@ const std::pair<std::vector<float2>, std::vector<float2>>& twiddles_cached(uint6
 
 }  // namespace
 
+// launch groups per submitted batch (Impl::serial): measured in profiles/README.md (round 3)
+constexpr int kDefaultSerial = 4;
+
 struct HipEngine::Impl {
   int device = 0;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;  // views of the current batch I/O slot
-  int batch = 4;
+  int batch = 4;                // templates per kernel launch (grid.y), each with its own FFT buffers
+  // Templates of one submitted batch run `serial` launch groups of `batch`
+  // templates back to back through the same FFT buffers: one completion event
+  // per submitted batch instead of one per group (an event record costs the
+  // stream ~7 us of idle GPU time; profiles/README.md round 3). BRP_SERIAL.
+  int serial = 1;
+  int slot_cap() const { return batch * serial; }  // templates per submitted batch
+  hipEvent_t prev_done = nullptr;  // completion event of the last completed batch (device-time statistics)
+  uint32_t key_base = 0;        // template index of the current launch group within its batch
+  bool group_reset = true;      // the current launch group zeroes the batch's candidate counter
   uint32_t cap = 1u << 20;      // candidate slots per batch (all templates and levels)
   uint32_t kcopy = 1024;        // slots copied back with every batch (more: second copy)
 
@@ -383,7 +395,7 @@ struct HipEngine::Impl {
     PinnedBuf<uint2> h_cands;
     uint8_t* h_in_p = nullptr;  // host view of the parameters (pinned copy or `in` itself)
     uint2* h_cands_p = nullptr;  // host view of the results (pinned copy or `cands` itself)
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;  // ev0: stage benchmark only; ev1: the batch's completion
     int nb = 0;
     bool pending = false;
   };
@@ -603,7 +615,7 @@ struct HipEngine::Impl {
         if (fg_in) return hipSuccess;  // the host wrote `in` directly
         return hipMemcpyAsync(in.p, h_in.p, thr_bytes + sizeof(TemplateDev) * nb, hipMemcpyHostToDevice, stream);
       case kPass1: {
-        if (bs) return bs_template_in(nb, &cands.p[0].x);
+        if (bs) return bs_template_in(nb, group_reset ? &cands.p[0].x : nullptr);
         hipk::Pass1Args a1{};
         a1.out = buf.p;
         a1.L2L3 = plan.L2 * plan.L3;
@@ -614,7 +626,7 @@ struct HipEngine::Impl {
         a1.n_unpadded = g.n_unpadded;
         a1.tmpl = tmpl.p;
         a1.partials = partials.p;
-        a1.reset = &cands.p[0].x;
+        a1.reset = group_reset ? &cands.p[0].x : nullptr;
         return hipk::launch_pass1(plan, hipk::P1_RESAMPLE, a1, nb, stream);
       }
       case kPass2: {
@@ -676,6 +688,7 @@ struct HipEngine::Impl {
         ah.xcd = hs_xcd;
         ah.pyr = pyr.p;
         ah.pyr_stride = hipk::hs_pyr_stride(ps_stride);
+        ah.key_base = key_base;
         return hipk::launch_harmonic_sum(ah, nb, stream);
       }
       case kEpilogue:
@@ -685,13 +698,29 @@ struct HipEngine::Impl {
     }
   }
 
-  // Enqueue the whole per-batch pipeline on `stream` (also used for capture).
+  // Enqueue the whole per-batch pipeline on `stream` (also used for capture):
+  // launch groups of up to `batch` templates back to back (passes 1-3 and the
+  // harmonic sum each), the parameter upload before the first group and the
+  // candidate read-back after the last. Each group reads its templates and
+  // thresholds at its offset in the batch's I/O slot and appends to the
+  // batch's one candidate list (keys carry the template's index in the batch).
   hipError_t enqueue(int nb) {
-    for (int st = 0; st < kNumStages; ++st) {
-      const hipError_t e = enqueue_stage(st, nb);
-      if (e != hipSuccess) return e;
+    TemplateDev* const tmpl0 = tmpl.p;
+    float* const thr0 = thr.p;
+    hipError_t e = enqueue_stage(kPrologue, nb);
+    for (int g0 = 0; e == hipSuccess && g0 < nb; g0 += batch) {
+      const int ng = std::min(batch, nb - g0);
+      tmpl.p = tmpl0 + g0;
+      thr.p = thr0 + static_cast<size_t>(g0) * hipk::kHsThrStride;
+      key_base = static_cast<uint32_t>(g0);
+      group_reset = g0 == 0;
+      for (int st = kPass1; e == hipSuccess && st <= kHarmonic; ++st) e = enqueue_stage(st, ng);
     }
-    return hipSuccess;
+    tmpl.p = tmpl0;
+    thr.p = thr0;
+    key_base = 0;
+    group_reset = true;
+    return e == hipSuccess ? enqueue_stage(kEpilogue, nb) : e;
   }
 };
 
@@ -819,6 +848,11 @@ int HipEngine::init(int device, int batch) {
   }
   impl_->device = device;
   impl_->batch = batch > 0 ? batch : 4;
+  {
+    const char* e = std::getenv("BRP_SERIAL");
+    const int sv = e ? std::atoi(e) : kDefaultSerial;
+    impl_->serial = std::max(1, std::min(sv, static_cast<int>(hipk::kHsMaxBatch) / impl_->batch));
+  }
   BRP_HIP_CHECK(hipStreamCreateWithFlags(&impl_->stream, hipStreamNonBlocking), RADPUL_HIP_DEVICE_SET);
   for (auto& o : impl_->io) {
     BRP_HIP_CHECK(hipEventCreate(&o.ev0), RADPUL_HIP_DEVICE_SET);
@@ -940,13 +974,14 @@ int HipEngine::setup_impl(const SearchGeometry& g, const float* host_series, con
     d.bs_h.release();
   }
   if ((rc = d.delta.alloc(B))) return rc;
-  if (B > hipk::kHsMaxBatch || g.fundamental_idx_hi >= (1u << hipk::kHsBinBits)) {
+  if (static_cast<size_t>(d.slot_cap()) > hipk::kHsMaxBatch || g.fundamental_idx_hi >= (1u << hipk::kHsBinBits)) {
     log_message(LOG_ERROR, true, "Batch %zu / fundamental_idx_hi %u beyond the candidate key packing.\n", B,
                 g.fundamental_idx_hi);
     return RADPUL_EVAL;
   }
-  d.thr_bytes = (B * hipk::kHsThrStride * sizeof(float) + 63) / 64 * 64;
-  const size_t in_bytes = d.thr_bytes + sizeof(TemplateDev) * B;
+  const size_t BS = static_cast<size_t>(d.slot_cap());  // templates per I/O slot
+  d.thr_bytes = (BS * hipk::kHsThrStride * sizeof(float) + 63) / 64 * 64;
+  const size_t in_bytes = d.thr_bytes + sizeof(TemplateDev) * BS;
   {
     const char* fg = std::getenv("BRP_FG");
     const std::string f = fg ? fg : "";
@@ -1269,8 +1304,8 @@ int HipEngine::process(const TemplateInput* t, int n, const float* thr, int thr_
   out.clear();
   out.resize(n);
   std::vector<TemplateCands> part;
-  for (int off = 0; off < n; off += d.batch) {
-    const int nb = std::min(d.batch, n - off);
+  for (int off = 0; off < n; off += d.slot_cap()) {
+    const int nb = std::min(d.slot_cap(), n - off);
     int rc = submit(t + off, nb, thr + static_cast<size_t>(off) * thr_stride, thr_stride);
     if (rc == 0) rc = complete(part);
     if (rc) return rc;
@@ -1287,7 +1322,7 @@ int HipEngine::max_in_flight() const {
 
 int HipEngine::submit(const TemplateInput* t, int nb, const float* thr, int thr_stride) {
   Impl& d = *impl_;
-  if (!d.ready || nb < 1 || nb > d.batch) return RADPUL_EMISC;
+  if (!d.ready || nb < 1 || nb > d.slot_cap()) return RADPUL_EMISC;
   if (!d.shared_series_valid()) {
     log_message(LOG_ERROR, true, "Pipeline reads a whitened series that was rewritten or freed since it was adopted.\n");
     return RADPUL_EVAL;
@@ -1334,7 +1369,8 @@ int HipEngine::submit(const TemplateInput* t, int nb, const float* thr, int thr_
     }
   }
   if (d.fg_in) std::atomic_thread_fence(std::memory_order_seq_cst);  // BAR writes before the launch
-  BRP_HIP_CHECK(hipEventRecord(d.ev0, d.stream), RADPUL_HIP_KERNEL_INVOKE);
+  // One event per batch, at its end: every event record leaves the stream idle
+  // for ~7 us (a start event cost 2-3 % of the bench, profiles/README.md round 3)
   if (use_graph) {
     BRP_HIP_CHECK(hipGraphLaunch(exec, d.stream), RADPUL_HIP_GRAPH);
   } else {
@@ -1361,8 +1397,11 @@ int HipEngine::complete(std::vector<TemplateCands>& out) {
   d.io_head = (slot + 1) % Impl::kIoSlots;
   trace::Range decode("brp:batch_decode");
   const int nb = o.nb;
+  // device time: from the end of the previous batch on this stream (its event
+  // is not re-recorded before this completion unless every slot is in flight)
   float ms = 0;
-  (void)hipEventElapsedTime(&ms, o.ev0, o.ev1);
+  if (d.prev_done != nullptr && max_in_flight() < Impl::kIoSlots) (void)hipEventElapsedTime(&ms, d.prev_done, o.ev1);
+  d.prev_done = d.io_busy() ? o.ev1 : nullptr;  // an idle stream restarts the chain
   d.st.gpu_ms += ms;
   d.st.batches += 1;
   if (d.shared_series != nullptr) d.st.shared_series_batches += 1;
@@ -1374,7 +1413,9 @@ int HipEngine::complete(std::vector<TemplateCands>& out) {
   }
   const uint2* src = o.h_cands_p + 1;
   std::vector<uint2> extra;
-  if (cnt > d.kcopy) {
+  // results in place (fine-grained memory): the whole list is host visible;
+  // a copied prefix of kcopy entries needs a second copy beyond that
+  if (!d.fg_out && cnt > d.kcopy) {
     extra.resize(cnt);
     // stream-ordered (a null-stream copy would invalidate another engine's
     // graph capture running in a sibling thread); waits for a batch queued
@@ -1560,7 +1601,7 @@ int HipEngine::bound_cells(int k, std::vector<float>& cells) {
 BackendStats HipEngine::stats() const { return impl_->st; }
 int HipEngine::device() const { return impl_->device; }
 const FFTPlan3& HipEngine::plan() const { return impl_->plan; }
-int HipEngine::batch() const { return impl_->batch; }
+int HipEngine::batch() const { return impl_->slot_cap(); }
 
 // ------------------------------------------------------------------ Backend
 namespace {

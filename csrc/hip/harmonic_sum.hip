@@ -138,7 +138,7 @@ __global__ void __launch_bounds__(kThreads) harmonic_sum_kernel(HSArgs a) {
     const int i = i0 + t;
     const bool in = t < TILE && (i >= w2 && i < fhi);
     const float p = in ? p0[it] : 0.0f;
-    emit(count, list, a.cap, in && p > thr0, hs_pack(b, 0, static_cast<uint32_t>(i)), p);
+    emit(count, list, a.cap, in && p > thr0, hs_pack(a.key_base + b, 0, static_cast<uint32_t>(i)), p);
   }
   // levels 1..4: group of 2^h consecutive i starting at s == 2^(h-1) mod 2^h;
   // one thread per group, stride-2^h reads made (nearly) conflict free by the
@@ -164,7 +164,7 @@ __global__ void __launch_bounds__(kThreads) harmonic_sum_kernel(HSArgs a) {
           pred = m > thr;
         }
       }
-      emit(count, list, a.cap, pred, hs_pack(b, h, static_cast<uint32_t>(j)), m);
+      emit(count, list, a.cap, pred, hs_pack(a.key_base + b, h, static_cast<uint32_t>(j)), m);
     }
   }
 }
@@ -660,7 +660,7 @@ __global__ void __launch_bounds__(256) hs_pruned_kernel(HSArgs a, uint32_t nblk)
     wave_sync();
     // level 0: the spectrum itself, indices of the block
     const bool in0 = act && li < kBlk && i >= w2 && i < fhi;
-    emit(count, list, a.cap, in0 && p0 > thr[0], hs_pack(b, 0, static_cast<uint32_t>(i)), p0);
+    emit(count, list, a.cap, in0 && p0 > thr[0], hs_pack(a.key_base + b, 0, static_cast<uint32_t>(i)), p0);
     // levels 1..4: lane li < 15 owns one group (8 of level 1, 4 of level 2, 2 of level 3, 1 of level 4)
     int h = 4, t0 = 0;
     if (li < 8) { h = 1; t0 = 2 * li + 1; }
@@ -675,7 +675,7 @@ __global__ void __launch_bounds__(256) hs_pruned_kernel(HSArgs a, uint32_t nblk)
       j = (ib + t0 + (g >> 1)) >> h;
       pred = j >= w2 && j < fhi && m > thr[h];
     }
-    emit(count, list, a.cap, pred, hs_pack(b, static_cast<uint32_t>(h), static_cast<uint32_t>(j)), m);
+    emit(count, list, a.cap, pred, hs_pack(a.key_base + b, static_cast<uint32_t>(h), static_cast<uint32_t>(j)), m);
     wave_sync();
   }
 }

@@ -37,6 +37,7 @@ struct HSArgs {
   bool xcd;     // pruned kernel: contiguous block ranges per XCD (BRP_HS_XCD=1, experiment)
   float* pyr;
   uint32_t pyr_stride;
+  uint32_t key_base;  // index of template 0 of this launch within the batch's candidate list
 };
 
 // cells covering the spectrum row, room for 4-bin cells (bins >= hhi count as 0)
