@@ -468,6 +468,7 @@ PYBIND11_MODULE(_brp, m) {
              return cands_to_list(out);
            })
       .def("max_in_flight", &HipEngine::max_in_flight)
+      .def("batch", &HipEngine::batch, "templates per submitted batch (launch-group size x BRP_SERIAL)")
       .def("adopt_series", [](HipEngine& e, const HipEngine& src) { check(e.adopt_series(src), "HipEngine.adopt_series"); })
       .def("power_spectrum",
            [](HipEngine& e, float P, float tau, float psi) {

@@ -172,8 +172,12 @@ constexpr bool kAblateP3Fft = true;
 constexpr bool kAblateP3Fft = false;
 #endif
 
+#ifndef BRP_P1_WAVES
+#define BRP_P1_WAVES 4  // waves per SIMD the register budget allows (build switch; 5 spills 24 B)
+#endif
 template <int R2>
-__global__ void __launch_bounds__(kNcol * 16) pass1_pruned3_kernel(Pass1Args a) {
+__global__ void __launch_bounds__(kNcol * 16) __attribute__((amdgpu_waves_per_eu(BRP_P1_WAVES, 8)))
+pass1_pruned3_kernel(Pass1Args a) {
   constexpr int L = 3 * R2 * 16;
   constexpr int TPC = 16;               // threads per column = butterfly groups of stages 1+2
   constexpr int NT = kNcol * TPC;

@@ -221,6 +221,36 @@ def test_engine_batches_in_flight_match_process(brp, gpu):
         eng.complete()  # nothing outstanding
 
 
+@pytest.mark.parametrize("batch,serial", [(1, 4), (2, 3), (1, 8)])
+def test_serial_launch_groups_match_single_templates(brp, gpu, monkeypatch, batch, serial):
+    """Serial launch groups (BRP_SERIAL): one submitted batch of batch x serial
+    templates runs its launch groups back to back through the same FFT buffers
+    into one candidate list (keys offset by the group's first template). Every
+    template's candidates equal those of one-template batches, bit for bit,
+    including a short last group."""
+    hdr, series, _ = brp.read_work_unit(str(WU))
+    opt = dict(OPT_BENCH, white=True)
+    geom = brp.derive_geometry(hdr, opt)
+    P, tau, psi = (x.astype(np.float32) for x in brp.read_template_bank(str(BANK)))
+    thr = [9.0, 12.0, 16.0, 22.0, 33.0]
+    n = batch * serial - 1  # the last launch group is short when batch > 1
+    monkeypatch.setenv("BRP_SERIAL", "1")
+    one = _engine(brp, geom, series, batch=1)
+    one.whiten(opt, brp.read_zaplist(str(ZAP)), series.copy())
+    assert one.batch() == 1
+    ref = [one.process(P[k:k + 1], tau[k:k + 1], psi[k:k + 1], thr)[0] for k in range(n)]
+    monkeypatch.setenv("BRP_SERIAL", str(serial))
+    grp = _engine(brp, geom, series, batch=batch)
+    grp.whiten(opt, brp.read_zaplist(str(ZAP)), series.copy())
+    assert grp.batch() == batch * serial
+    got = grp.process(P[:n], tau[:n], psi[:n], thr)
+    assert sum(len(ref[k][h][0]) for k in range(n) for h in range(5)) > 0
+    for k in range(n):
+        for h in range(5):
+            np.testing.assert_array_equal(got[k][h][0], ref[k][h][0])
+            np.testing.assert_array_equal(got[k][h][1], ref[k][h][1])
+
+
 def test_whitening_wide_window_matches_cpu(brp, gpu, tmp_path):
     """-B above the LDS kernel's 3072: whitening stays on the device (wide
     running median) and matches the CPU whitening."""
