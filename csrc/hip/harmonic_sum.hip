@@ -404,28 +404,37 @@ struct HsDirect {
   // largest hi - lo over all blocks for a span of N indices
   static constexpr int kD16 = ((((L * (kBlk - 1) + 15) / 16) + (1 << K) - 1) >> K);
   static constexpr int kD20 = ((((L * (kBlkSpan - 1) + 15) / 16) + (1 << K) - 1) >> K);
-  static_assert((kTail ? kD20 : kD16) <= 3, "one 4-entry load per harmonic");
+  static_assert((kTail ? kD20 : kD16) <= 3, "one load of at most 4 entries per harmonic");
   static constexpr int kIn = ((15 * L) / 16) >> K;  // entries e <= kIn lie in [lo, h16] for every block
+  static constexpr int kN = (kTail ? kD20 : kD16) + 1;  // entries a block can reach (1..4)
 };
 
-using f4u = float __attribute__((ext_vector_type(4), aligned(4)));
+// N consecutive floats from a dword-aligned address as one load
+template <int N>
+using fvu = float __attribute__((ext_vector_type(N), aligned(4)));
+using f4u = fvu<4>;
 
-// the 4 entries from lo of harmonic kHarm[Q] (dword-aligned 16-byte load)
+// the entries from lo of harmonic kHarm[Q] a block can reach, as one load of
+// exactly that many dwords (45 instead of 64 VGPRs for the 16 harmonics)
 template <int CK, int Q, int MODE>
 __device__ __forceinline__ f4u hs_direct_load(const PsT<MODE>* P, const float* C8, int32_t ib) {
   using H = HsDirect<CK, Q>;
   const uint32_t lo = hs_cell(H::L, H::K, ib);
+  f4u v = {0.0f, 0.0f, 0.0f, 0.0f};
   if constexpr (H::K > 0 || MODE == HS_F32) {
-    const float* src = H::K > 0 ? C8 : reinterpret_cast<const float*>(P);
-    return *reinterpret_cast<const f4u*>(src + lo);
+    const float* src = (H::K > 0 ? C8 : reinterpret_cast<const float*>(P)) + lo;
+    if constexpr (H::kN == 1) {
+      v.x = *src;
+    } else {
+      const fvu<H::kN> w = *reinterpret_cast<const fvu<H::kN>*>(src);
+#pragma unroll
+      for (int e = 0; e < H::kN; ++e) v[e] = w[e];
+    }
   } else {
-    f4u v;
-    v.x = static_cast<float>(P[lo]);
-    v.y = static_cast<float>(P[lo + 1]);
-    v.z = static_cast<float>(P[lo + 2]);
-    v.w = static_cast<float>(P[lo + 3]);
-    return v;
+#pragma unroll
+    for (int e = 0; e < H::kN; ++e) v[e] = static_cast<float>(P[lo + e]);
   }
+  return v;
 }
 
 // maxima over the block's 16 indices (m16) and, for the first 8 harmonics,
