@@ -383,6 +383,26 @@ int SearchSession::run(uint32_t begin, uint32_t end, CandidateTable& table, Sear
   table.thresholds(g.chi2_thr, thr_shared);
   std::atomic<uint32_t> next_first{begin};
   std::atomic<bool> stop{false};
+  // Batch sizes shrink over the last templates of the range (below two
+  // batches per in-flight slot of all pipelines) so that the pipelines finish
+  // together: a shard's tail then idles the GPU for about one template instead
+  // of one full batch (serial launch groups make batches 4 templates long).
+  int slots_all = 0;
+  for (auto& be : d.backends) slots_all += std::max(1, be->max_in_flight());
+  auto take = [&](uint32_t& first) -> int {
+    uint32_t f = next_first.load();
+    for (;;) {
+      if (f >= end) return 0;
+      const uint32_t rem = end - f;
+      const uint32_t n = std::min<uint32_t>(
+          std::min<uint32_t>(static_cast<uint32_t>(B), rem),
+          std::max<uint32_t>(1u, rem / static_cast<uint32_t>(2 * std::max(1, slots_all))));
+      if (next_first.compare_exchange_weak(f, f + n)) {
+        first = f;
+        return static_cast<int>(n);
+      }
+    }
+  };
   // Each worker keeps up to max_in_flight() batches of its backend submitted
   // (the next batch is launched while the previous one runs), completing them
   // in submission order.
@@ -402,9 +422,9 @@ int SearchSession::run(uint32_t begin, uint32_t end, CandidateTable& table, Sear
         // finish inside their critical section (demod_binary.c:1241-1296)
         boinc::suspend_point();
         if (stop.load()) break;
-        const uint32_t first = next_first.fetch_add(static_cast<uint32_t>(B));
-        if (first >= end) break;
-        const int n = static_cast<int>(std::min<uint32_t>(B, end - first));
+        uint32_t first = 0;
+        const int n = take(first);
+        if (n == 0) break;
         float thr[kNumHarmonicLevels];
         {
           std::lock_guard<std::mutex> lk(mu);
