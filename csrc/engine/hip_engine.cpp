@@ -319,6 +319,10 @@ struct HipEngine::Impl {
   bool group_reset = true;      // the current launch group zeroes the batch's candidate counter
   uint32_t cap = 1u << 20;      // candidate slots per batch (all templates and levels)
   uint32_t kcopy = 1024;        // slots copied back with every batch (more: second copy)
+  // results in place (fg_out): longer lists are DMA-copied instead of read over
+  // the PCIe BAR (uncached host reads; config 4 measured 12.8k vs 17.4k pairs/s
+  // reading every list in place). BRP_FG_INPLACE_MAX, at most kcopy.
+  uint32_t inplace_max = 1024;
 
   SearchGeometry g;
   FFTPlan3 plan;
@@ -960,6 +964,8 @@ int HipEngine::setup_impl(const SearchGeometry& g, const float* host_series, con
   if ((rc = d.ps.alloc(B * d.ps_stride))) return rc;
   d.hs_prune = std::getenv("BRP_HS_FULL") == nullptr || std::atoi(std::getenv("BRP_HS_FULL")) == 0;
   d.hs_cell_shift = (std::getenv("BRP_HS_CELL") && std::atoi(std::getenv("BRP_HS_CELL")) == 4) ? 2 : 3;
+  if (const char* e = std::getenv("BRP_FG_INPLACE_MAX"))
+    d.inplace_max = std::min<uint32_t>(d.kcopy, static_cast<uint32_t>(std::max(0, std::atoi(e))));
   d.hs_direct = std::getenv("BRP_HS_DIRECT") == nullptr || std::atoi(std::getenv("BRP_HS_DIRECT")) != 0;
   d.hs_xcd = std::getenv("BRP_HS_XCD") != nullptr && std::atoi(std::getenv("BRP_HS_XCD")) == 1;
   if ((rc = d.pyr.alloc(B * hipk::hs_pyr_stride(d.ps_stride)))) return rc;
@@ -1413,9 +1419,9 @@ int HipEngine::complete(std::vector<TemplateCands>& out) {
   }
   const uint2* src = o.h_cands_p + 1;
   std::vector<uint2> extra;
-  // results in place (fine-grained memory): the whole list is host visible;
-  // a copied prefix of kcopy entries needs a second copy beyond that
-  if (!d.fg_out && cnt > d.kcopy) {
+  // beyond kcopy entries a DMA copy of the list beats reading it in place
+  // (uncached reads over the PCIe BAR) or a second copied prefix
+  if (cnt > (d.fg_out ? d.inplace_max : d.kcopy)) {
     extra.resize(cnt);
     // stream-ordered (a null-stream copy would invalidate another engine's
     // graph capture running in a sibling thread); waits for a batch queued
