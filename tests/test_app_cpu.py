@@ -243,3 +243,21 @@ def test_app_no_checkpoint_and_progress_every(app, case, tmp_path):
     r = _run_app(app, _app_args(case, cut, extra), cut, BRP_CHECKPOINT_PERIOD="0", BRP_FAULT="kill_after_template:5")
     assert r.returncode == 0, r.stderr[-2000:]
     assert not (cut / "cp.cpt").exists() and not (cut / "res.cand").exists()
+
+
+@pytest.mark.parametrize("batch,workers", [(4, 3), (3, 2), (1, 4)])
+def test_session_table_independent_of_batching(brp, case, tmp_path, batch, workers):
+    """SearchSession.run deals batches to its workers (shrinking the last ones
+    so the pipelines finish together) and applies them in template order: the
+    candidate table is byte-identical to one worker with one-template batches
+    (demod_binary.c:1180-1443 sequential semantics)."""
+    def table(b, w):
+        opts = _cfg(case, tmp_path, batch=b).options()
+        s = brp.SearchSession()
+        s.open(opts, w, [])
+        s.prepare()
+        t, _ = s.run(0, s.total(), brp.CandidateTable())
+        return bytes(t.to_bytes())
+
+    ref = table(1, 1)
+    assert table(batch, workers) == ref
