@@ -34,14 +34,101 @@ __global__ void whiten_power_kernel(const float2* spec, uint32_t n, float* ps) {
 // load (the same address for every lane: a broadcast) and counts members
 // branch-free, leaving the loop once every lane of the wave has found its
 // median; the plain scan waits on one dependent 2-byte LDS load per entry.
-template <int SPAN, int NT, bool CHUNKED>
+// order-preserving bits of a float (any non-NaN value; -0 sorts below +0)
+__device__ __forceinline__ uint32_t ord_bits(float f) {
+  const uint32_t b = __float_as_uint(f);
+  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+__device__ __forceinline__ float unord_bits(uint32_t o) {
+  return __uint_as_float((o & 0x80000000u) ? (o & 0x7fffffffu) : ~o);
+}
+
+// REG: the span is sorted as 48-bit (ordered key, position) words, 16 per
+// thread (element 16 t + j): bitonic stages with strides below 16 in
+// registers, strides within a wave through cross-lane shuffles, and only the
+// 3 cross-wave passes through LDS -- instead of 78 LDS passes of 2048
+// compare-exchanges (which were most of the kernel's time).
+template <int SPAN, int NT>
+__device__ __forceinline__ void rmed_sort_reg(const float* in, uint32_t n_in, uint32_t W, uint32_t o0,
+                                              uint32_t per_block, float* key, uint16_t* pos, uint16_t* rank) {
+  static_assert(SPAN == 16 * NT, "16 elements per thread");
+  const int t = threadIdx.x;
+  uint64_t v[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int e = 16 * t + j;
+    const uint32_t g = o0 + e;
+    const float k = (e < static_cast<int>(per_block + W - 1) && g < n_in) ? in[g] : __builtin_inff();
+    v[j] = (static_cast<uint64_t>(ord_bits(k)) << 16) | static_cast<uint32_t>(e);
+  }
+  uint32_t* keyu = reinterpret_cast<uint32_t*>(key);
+#pragma unroll
+  for (int size = 2; size <= SPAN; size <<= 1) {
+#pragma unroll
+    for (int d = size >> 1; d > 0; d >>= 1) {
+      if (d >= 16) {
+        const int k = d >> 4;                      // partner thread t ^ k holds element e ^ d
+        const bool asc = ((16 * t) & size) == 0;   // size >= 32
+        const bool keep_min = ((t & k) == 0) == asc;
+        if (k < kWave) {
+#pragma unroll
+          for (int j = 0; j < 16; ++j) {
+            const uint32_t lo = __shfl_xor(static_cast<uint32_t>(v[j]), k, kWave);
+            const uint32_t hi = __shfl_xor(static_cast<uint32_t>(v[j] >> 32), k, kWave);
+            const uint64_t w = (static_cast<uint64_t>(hi) << 32) | lo;
+            v[j] = keep_min ? (w < v[j] ? w : v[j]) : (w > v[j] ? w : v[j]);
+          }
+        } else {
+          __syncthreads();  // the previous exchange has been read
+#pragma unroll
+          for (int j = 0; j < 16; ++j) {
+            keyu[16 * t + j] = static_cast<uint32_t>(v[j] >> 16);
+            pos[16 * t + j] = static_cast<uint16_t>(v[j]);
+          }
+          __syncthreads();
+#pragma unroll
+          for (int j = 0; j < 16; ++j) {
+            const int q = (16 * t + j) ^ d;
+            const uint64_t w = (static_cast<uint64_t>(keyu[q]) << 16) | pos[q];
+            v[j] = keep_min ? (w < v[j] ? w : v[j]) : (w > v[j] ? w : v[j]);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          if ((j & d) != 0) continue;
+          const int p = j | d;
+          const bool asc = ((16 * t + j) & size) == 0;
+          const uint64_t a = v[j], b = v[p];
+          const uint64_t mn = a < b ? a : b, mx = a < b ? b : a;
+          v[j] = asc ? mn : mx;
+          v[p] = asc ? mx : mn;
+        }
+      }
+    }
+  }
+  __syncthreads();  // the last exchange has been read
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int e = 16 * t + j;
+    key[e] = unord_bits(static_cast<uint32_t>(v[j] >> 16));
+    pos[e] = static_cast<uint16_t>(v[j]);
+    rank[static_cast<uint16_t>(v[j])] = static_cast<uint16_t>(e);
+  }
+  __syncthreads();
+}
+
+template <int SPAN, int NT, bool CHUNKED, bool REG = false>
 __global__ void __launch_bounds__(NT) running_median_kernel(const float* in, uint32_t n_in, uint32_t W, float* med,
                                                             uint32_t n_out, uint32_t per_block) {
-  __shared__ float key[SPAN];
+  __shared__ __attribute__((aligned(16))) float key[SPAN];
   __shared__ __attribute__((aligned(16))) uint16_t pos[SPAN];
   __shared__ uint16_t rank[SPAN];
   static_assert(SPAN <= 65536, "16-bit positions");
   const uint32_t o0 = blockIdx.x * per_block;
+  if constexpr (REG) {
+    rmed_sort_reg<SPAN, NT>(in, n_in, W, o0, per_block, key, pos, rank);
+  } else {
   for (int t = threadIdx.x; t < SPAN; t += NT) {
     const uint32_t g = o0 + t;
     key[t] = (t < static_cast<int>(per_block + W - 1) && g < n_in) ? in[g] : __builtin_inff();
@@ -69,6 +156,7 @@ __global__ void __launch_bounds__(NT) running_median_kernel(const float* in, uin
   }
   for (int e = threadIdx.x; e < SPAN; e += NT) rank[pos[e]] = static_cast<uint16_t>(e);
   __syncthreads();
+  }
 
   const uint32_t mid = (W + (W & 1)) / 2 - 1;  // 0-based order statistic of the lower middle
   const bool odd = (W & 1) != 0;
@@ -210,7 +298,13 @@ hipError_t launch_running_median(const float* in, uint32_t n_in, uint32_t W, flo
   constexpr int kSpan = 4096, kThreads = 256;
   const uint32_t per = kSpan - W + 1;
   static const bool plain = std::getenv("BRP_RMED_PLAIN") != nullptr;  // A/B switch
-  if (plain)
+  // register/shuffle sort by default (655 -> 503 us per whitening median on
+  // MI355X, bit-exact; profiles/README.md round 3); BRP_RMED_REG=0: LDS bitonic
+  static const bool reg = std::getenv("BRP_RMED_REG") == nullptr || std::atoi(std::getenv("BRP_RMED_REG")) != 0;
+  if (reg && !plain)
+    hipLaunchKernelGGL((running_median_kernel<kSpan, kThreads, true, true>), dim3((n_out + per - 1) / per),
+                       dim3(kThreads), 0, s, in, n_in, W, med, n_out, per);
+  else if (plain)
     hipLaunchKernelGGL((running_median_kernel<kSpan, kThreads, false>), dim3((n_out + per - 1) / per), dim3(kThreads), 0,
                        s, in, n_in, W, med, n_out, per);
   else
