@@ -118,9 +118,12 @@ __device__ __forceinline__ void rmed_sort_reg(const float* in, uint32_t n_in, ui
   __syncthreads();
 }
 
+// walkers: threads that walk the window (runs of per_block / walkers outputs
+// each); every walker first scans the sorted span for its first median, so
+// fewer, longer runs trade that scan against the sequential walk
 template <int SPAN, int NT, bool CHUNKED, bool REG = false>
 __global__ void __launch_bounds__(NT) running_median_kernel(const float* in, uint32_t n_in, uint32_t W, float* med,
-                                                            uint32_t n_out, uint32_t per_block) {
+                                                            uint32_t n_out, uint32_t per_block, uint32_t walkers = NT) {
   __shared__ __attribute__((aligned(16))) float key[SPAN];
   __shared__ __attribute__((aligned(16))) uint16_t pos[SPAN];
   __shared__ uint16_t rank[SPAN];
@@ -160,7 +163,7 @@ __global__ void __launch_bounds__(NT) running_median_kernel(const float* in, uin
 
   const uint32_t mid = (W + (W & 1)) / 2 - 1;  // 0-based order statistic of the lower middle
   const bool odd = (W & 1) != 0;
-  const uint32_t run = (per_block + NT - 1) / NT;
+  const uint32_t run = (per_block + walkers - 1) / walkers;
   const uint32_t t0 = threadIdx.x * run;
   uint32_t t1 = min(t0 + run, per_block);
   if (o0 + t1 > n_out) t1 = n_out > o0 ? n_out - o0 : 0;
@@ -330,12 +333,14 @@ hipError_t launch_running_median(const float* in, uint32_t n_in, uint32_t W, flo
   constexpr int kSpan = 4096, kThreads = 256;
   const uint32_t per = kSpan - W + 1;
   static const bool plain = std::getenv("BRP_RMED_PLAIN") != nullptr;  // A/B switch
+  static const int walkers_env = std::getenv("BRP_RMED_WALKERS") ? std::atoi(std::getenv("BRP_RMED_WALKERS")) : 0;
+  const uint32_t walkers = static_cast<uint32_t>(walkers_env > 0 ? std::min(kThreads, walkers_env) : kThreads);
   // register/shuffle sort by default (655 -> 503 us per whitening median on
   // MI355X, bit-exact; profiles/README.md round 3); BRP_RMED_REG=0: LDS bitonic
   static const bool reg = std::getenv("BRP_RMED_REG") == nullptr || std::atoi(std::getenv("BRP_RMED_REG")) != 0;
   if (reg && !plain)
     hipLaunchKernelGGL((running_median_kernel<kSpan, kThreads, true, true>), dim3((n_out + per - 1) / per),
-                       dim3(kThreads), 0, s, in, n_in, W, med, n_out, per);
+                       dim3(kThreads), 0, s, in, n_in, W, med, n_out, per, walkers);
   else if (plain)
     hipLaunchKernelGGL((running_median_kernel<kSpan, kThreads, false>), dim3((n_out + per - 1) / per), dim3(kThreads), 0,
                        s, in, n_in, W, med, n_out, per);
