@@ -389,8 +389,17 @@ int SearchSession::run(uint32_t begin, uint32_t end, CandidateTable& table, Sear
   // of one full batch (serial launch groups make batches 4 templates long).
   int slots_all = 0;
   for (auto& be : d.backends) slots_all += std::max(1, be->max_in_flight());
+  const uint32_t tail = 2u * static_cast<uint32_t>(std::max(1, slots_all)) * static_cast<uint32_t>(B);
   auto take = [&](uint32_t& first) -> int {
-    uint32_t f = next_first.load();
+    uint32_t f = next_first.load(std::memory_order_relaxed);
+    if (f < end && end - f > tail + static_cast<uint32_t>(B)) {
+      // far from the tail: one fetch_add (a CAS loop contends when many
+      // pipelines take batches at once); one landing in the tail is still exact
+      f = next_first.fetch_add(static_cast<uint32_t>(B));
+      if (f >= end) return 0;
+      first = f;
+      return static_cast<int>(std::min<uint32_t>(static_cast<uint32_t>(B), end - f));
+    }
     for (;;) {
       if (f >= end) return 0;
       const uint32_t rem = end - f;
