@@ -121,13 +121,68 @@ def recall_vs_golden(table, geom) -> dict | None:
     return rec
 
 
+def launch_ranks(args) -> int:
+    """`--gpus N` (N > 1) without a launcher environment: start the N rank
+    processes here, one per GPU, the way torch.distributed.run would
+    (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT).
+    Nothing in this process touches the GPU (device_count does not initialise
+    HIP), so no rank inherits a HIP context. Rank 0 prints the JSON line.
+    Fewer visible devices than N is an error, never a silent 1-GPU run."""
+    import socket
+    import subprocess
+
+    n = args.gpus
+    if not args.cpu:
+        import torch
+
+        have = torch.cuda.device_count()
+        if have < n:
+            print(f"[bench] error: --gpus {n} but only {have} HIP device(s) are visible", file=sys.stderr)
+            return 2
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), BRP_BENCH_LAUNCHED="1")
+        procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve()), *sys.argv[1:]], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                print(f"[bench] rank process {procs.index(p)} exited with {code}; stopping the others",
+                      file=sys.stderr, flush=True)
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    for p in procs:
+        p.wait()
+    return rc
+
+
 def main() -> int:
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ and not args.shard_of:
+        return launch_ranks(args)
     import torch  # noqa: F401  (loads the HIP runtime first; RCCL backend)
 
     from boinc_app_eah_brp_amd import native
     from boinc_app_eah_brp_amd.parallel import ShardedSearch, barrier, init_distributed, max_over_ranks
 
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if not args.shard_of and world_env != args.gpus:
+        print(f"[bench] error: --gpus {args.gpus} but WORLD_SIZE={world_env}", file=sys.stderr)
+        return 2
+    if not args.cpu and not args.shard_of and torch.cuda.device_count() < world_env:
+        print(f"[bench] error: {world_env} ranks but only {torch.cuda.device_count()} HIP device(s)", file=sys.stderr)
+        return 2
     ctx = init_distributed("gloo" if args.cpu else None)
     if args.shard_of:
         from boinc_app_eah_brp_amd.parallel import DistContext
@@ -136,8 +191,6 @@ def main() -> int:
         ctx = DistContext(rank=r_of, world=n_of, local_rank=ctx.local_rank, backend="none", solo_shard=True)
     use_gpu = torch.cuda.is_available() and not args.cpu
     world = 1 if ctx.solo_shard else ctx.world
-    if world != args.gpus and ctx.rank == 0:
-        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}", file=sys.stderr)
     brp = native()
     brp.set_log_level(2)
     wu, bank, zap = WU, BANK, ZAP
@@ -238,6 +291,9 @@ def main() -> int:
             "recall_vs_golden": rec,
             "candidates_in_table": n_cands,
             "collective_failure_degraded": ctx.degraded,
+            "floor_sync_rounds_last_step": getattr(search, "floor_rounds", None),
+            "launched_by": "bench.py" if os.environ.get("BRP_BENCH_LAUNCHED") else
+                           ("torch.distributed.run" if world > 1 else "single process"),
             "table_identical_to_warmup": (first == bytes(table.to_bytes())) if first is not None else None,
             "gpu_ms_rank0": round(stats["gpu_ms"], 3),
             "whiten_ms_rank0": round(stats["whiten_ms"], 3),

@@ -49,6 +49,7 @@ class SearchOutput:
     templates_run: int
     interrupted: bool
     timings: dict = field(default_factory=dict)
+    stats: dict = field(default_factory=dict)  # backend counters (bounded-output re-runs, ...)
 
     def candidates(self):
         """Table entries (f0 bin, power, P_b, tau, Psi, n_harm) with n_harm > 0."""
@@ -70,7 +71,9 @@ class BRPSearch:
         return SearchOutput(table=r["table"], geometry=r["geometry"], templates_total=r["templates_total"],
                             templates_run=r["templates_run"], interrupted=r["interrupted"],
                             timings=dict(setup=r["t_setup"], templates=r["t_templates"], total=r["t_total"],
-                                         gpu_ms=r["gpu_ms"], whiten_ms=r["whiten_ms"]))
+                                         gpu_ms=r["gpu_ms"], whiten_ms=r["whiten_ms"]),
+                            stats=dict(overflow_reruns=r["overflow_reruns"], select_batches=r["select_batches"],
+                                       select_exits=r["select_exits"]))
 
     def results(self):
         lines, done = self.brp.read_results(self.config.outputfile)

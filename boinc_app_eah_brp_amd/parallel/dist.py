@@ -204,6 +204,63 @@ def max_floors_over_ranks(floors: list[float], ctx: DistContext) -> list[float]:
     return [float(v) for v in t.cpu().tolist()]
 
 
+def floor_sync_interval_s() -> float:
+    """Seconds between floor exchanges while a shard runs (BRP_FLOOR_SYNC_MS,
+    default 5; 0 disables the exchange)."""
+    return float(os.environ.get("BRP_FLOOR_SYNC_MS", "5")) / 1e3
+
+
+class FloorSync:
+    """Global pruning while every rank searches its shard.
+
+    A helper thread all-reduces (max) the five level floors of this rank's
+    running table, together with a "still running" flag, over a gloo side
+    group, and raises the session's external floors with the result: the
+    device thresholds of every rank become the largest 100th-place power any
+    rank has reached (demod_binary.c:1268-1282 semantics). That is a valid lower
+    bound of the merged table's floor (every rank's 100 entries of a level are
+    distinct bins the merge also holds at >= that power), so the filtered bins
+    can never enter the merged table. Ranks keep exchanging until the flag is
+    clear on all of them, so every rank makes the same number of calls and
+    they all leave the loop on the same round."""
+
+    def __init__(self, session, ctx: DistContext, group, interval_s: float):
+        self.session, self.ctx, self.group, self.interval = session, ctx, group, interval_s
+        self.running = True
+        self.rounds = 0
+        self.error: Exception | None = None
+        self.thread = None
+
+    def start(self) -> "FloorSync":
+        import threading
+
+        self.thread = threading.Thread(target=self._loop, name="brp-floor-sync", daemon=True)
+        self.thread.start()
+        return self
+
+    def _loop(self) -> None:
+        import torch
+        import torch.distributed as dist
+
+        try:
+            while True:
+                f = list(self.session.local_floors())
+                t = torch.tensor(f + [1.0 if self.running else 0.0], dtype=torch.float64)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+                self.rounds += 1
+                self.session.raise_external_floors([float(v) for v in t[:5].tolist()])
+                if t[5].item() == 0.0:
+                    return
+                time.sleep(self.interval)
+        except Exception as e:  # peer gone / timeout: the table all-gather reports it
+            self.error = e
+
+    def finish(self) -> None:
+        self.running = False
+        if self.thread is not None:
+            self.thread.join()
+
+
 def barrier(ctx: DistContext) -> None:
     if ctx.distributed:
         import torch.distributed as dist
@@ -241,18 +298,36 @@ class ShardedSearch:
         self.total = self.session.total()
         self.begin, self.end = shard_range(self.total, ctx.rank, ctx.world)
         self.timings: dict = {}  # accumulated seconds per phase of step()
+        self.floor_interval = floor_sync_interval_s()
+        self.floor_group = None
+        self.floor_rounds = 0  # exchanges of the last step (tests, bench JSON)
+        if ctx.distributed and self.floor_interval > 0:
+            import torch.distributed as dist
+
+            # CPU side group: the exchange never queues RCCL kernels beside the search
+            self.floor_group = dist.new_group(backend="gloo", timeout=timedelta(seconds=collective_timeout_s()))
 
     def step(self, limit: int | None = None):
-        """Whiten + search this rank's shard + all-gather + merge. Returns the merged table."""
+        """Whiten + search this rank's shard (exchanging level floors with the
+        other ranks while it runs) + all-gather + merge. Returns the merged table."""
         total = self.total if limit is None else min(limit, self.total)
         t0 = time.perf_counter()
+        self.session.reset_external_floors()  # every step is an independent search
         self.session.prepare()
         t1 = time.perf_counter()
         search_s = [0.0]
 
         def run_shard(begin, end):
             ts = time.perf_counter()
-            table, _ = self.session.run(begin, end, self.brp.CandidateTable())
+            sync = None
+            if self.floor_group is not None and self.ctx.distributed:
+                sync = FloorSync(self.session, self.ctx, self.floor_group, self.floor_interval).start()
+            try:
+                table, _ = self.session.run(begin, end, self.brp.CandidateTable())
+            finally:
+                if sync is not None:
+                    sync.finish()
+                    self.floor_rounds = sync.rounds
             search_s[0] += time.perf_counter() - ts
             return [table]
 

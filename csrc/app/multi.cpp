@@ -82,6 +82,9 @@ BackendStats MultiSession::stats() const {
     t.templates += s.templates;
     t.batches += s.batches;
     t.overflow_reruns += s.overflow_reruns;
+    t.select_batches += s.select_batches;
+    t.select_exits += s.select_exits;
+    t.list_dma_copies += s.list_dma_copies;
     t.shared_series_batches += s.shared_series_batches;
     t.peer_series_copies += s.peer_series_copies;
   }

@@ -150,7 +150,51 @@ struct SearchSession::Impl {
   std::vector<std::unique_ptr<Backend>> backends;
   std::vector<float> series;  // whitened (or raw) series used for templates
   std::shared_ptr<void> wu_pin;  // wu.samples page-locked for the per-pass upload (released first)
+  // floors of the table being applied (published after every batch) and the
+  // external (other ranks') floors; float bits in atomics
+  std::atomic<uint32_t> own_floor[kNumHarmonicLevels] = {};
+  std::atomic<uint32_t> ext_floor[kNumHarmonicLevels] = {};
+  void publish_floors(const CandidateTable& t) {
+    for (int h = 0; h < kNumHarmonicLevels; ++h) {
+      const float f = static_cast<float>(t.floor_power(h));
+      uint32_t b;
+      std::memcpy(&b, &f, sizeof(b));
+      own_floor[h].store(b, std::memory_order_relaxed);
+    }
+  }
+  float ext(int h) const {
+    const uint32_t b = ext_floor[h].load(std::memory_order_relaxed);
+    float f;
+    std::memcpy(&f, &b, sizeof(f));
+    return f;
+  }
 };
+
+void SearchSession::local_floors(float out[kNumHarmonicLevels]) const {
+  for (int h = 0; h < kNumHarmonicLevels; ++h) {
+    const uint32_t b = impl_->own_floor[h].load(std::memory_order_relaxed);
+    std::memcpy(&out[h], &b, sizeof(float));
+  }
+}
+
+void SearchSession::raise_external_floors(const float f[kNumHarmonicLevels]) {
+  for (int h = 0; h < kNumHarmonicLevels; ++h) {
+    // non-negative floats order like their bit patterns: an atomic max on the bits
+    if (!(f[h] > 0.0f)) continue;
+    uint32_t b;
+    std::memcpy(&b, &f[h], sizeof(b));
+    uint32_t cur = impl_->ext_floor[h].load(std::memory_order_relaxed);
+    while (b > cur && !impl_->ext_floor[h].compare_exchange_weak(cur, b, std::memory_order_relaxed)) {
+    }
+  }
+}
+
+void SearchSession::reset_external_floors() {
+  for (int h = 0; h < kNumHarmonicLevels; ++h) {
+    impl_->ext_floor[h].store(0, std::memory_order_relaxed);
+    impl_->own_floor[h].store(0, std::memory_order_relaxed);
+  }
+}
 
 SearchSession::SearchSession() : impl_(new Impl) {}
 SearchSession::~SearchSession() = default;
@@ -169,6 +213,9 @@ BackendStats SearchSession::stats() const {
     t.templates += s.templates;
     t.batches += s.batches;
     t.overflow_reruns += s.overflow_reruns;
+    t.select_batches += s.select_batches;
+    t.select_exits += s.select_exits;
+    t.list_dma_copies += s.list_dma_copies;
     t.shared_series_batches += s.shared_series_batches;
     t.peer_series_copies += s.peer_series_copies;
   }
@@ -237,14 +284,13 @@ int SearchSession::open(const SearchOptions& opt, const SearchControl& ctl) {
     return 0;
   }
   if (!d.opt.use_cpu && !hip_backend_supports(d.g)) {
-    // FFTW accepts any length; the HIP FFT is compiled for N/2 = L1*L2*L3 over
-    // 16*2^a*3^b*5^c lengths. Other paddings run on the CPU golden model.
-    const int nt = std::max(1, std::min(64, static_cast<int>(std::thread::hardware_concurrency())));
-    log_message(LOG_WARN, true,
-                "No HIP FFT plan for N = %u (padding %.3f): using the CPU backend with %d threads.\n", d.g.nsamples,
-                d.opt.padding, nt);
-    d.opt.use_cpu = true;
-    ngpu = nt;
+    // Every N the reference can form on a real work unit has a plan: the
+    // three-pass FFT for N/2 = L1*L2*L3 over 16*2^a*3^b*5^c lengths, the chirp-z
+    // transform over such a length for all others (convolution length < 2^31,
+    // i.e. N < ~2^30). Beyond that the product path refuses loudly; it never
+    // switches to the CPU golden model behind the user's back.
+    log_message(LOG_ERROR, true, "No HIP FFT plan for N = %u (padding %.3f).\n", d.g.nsamples, d.opt.padding);
+    return RADPUL_HIP_FFT_PLAN;
   }
   // HIP: ctl.pipelines backends per device, consecutive backends on one device
   const int per_dev = d.opt.use_cpu ? 1 : std::max(1, ctl.pipelines);
@@ -381,6 +427,7 @@ int SearchSession::run(uint32_t begin, uint32_t end, CandidateTable& table, Sear
   std::map<uint32_t, BatchResult> ready;
   float thr_shared[kNumHarmonicLevels];
   table.thresholds(g.chi2_thr, thr_shared);
+  d.publish_floors(table);
   std::atomic<uint32_t> next_first{begin};
   std::atomic<bool> stop{false};
   // Batch sizes shrink over the last templates of the range (below two
@@ -439,6 +486,7 @@ int SearchSession::run(uint32_t begin, uint32_t end, CandidateTable& table, Sear
           std::lock_guard<std::mutex> lk(mu);
           std::memcpy(thr, thr_shared, sizeof(thr));
         }
+        for (int h = 0; h < kNumHarmonicLevels; ++h) thr[h] = std::fmax(thr[h], d.ext(h));
         boinc::begin_critical_section();
         const int rc = be->submit(&d.tin[first], n, thr);
         if (rc) {
@@ -517,6 +565,7 @@ int SearchSession::run(uint32_t begin, uint32_t end, CandidateTable& table, Sear
       std::lock_guard<std::mutex> lk(mu);
       table.thresholds(g.chi2_thr, thr_shared);
     }
+    d.publish_floors(table);
   }
   stop.store(true);
   for (auto& th : threads) th.join();

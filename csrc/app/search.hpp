@@ -66,6 +66,17 @@ class SearchSession {
   const SearchOptions& options() const;
   uint32_t total() const;
   BackendStats stats() const;
+  // Global pruning across ranks (parallel/dist.py FloorSync): level floors
+  // (100th power, 0 while a level is not full) of the table the running
+  // run() applies to, and lower bounds of the *merged* table's floors that
+  // other ranks reported. Device thresholds become max(chi2, own floor,
+  // external floor); the table itself is applied with its own thresholds, so
+  // only bins that can never reach the merged table are filtered out
+  // (demod_binary.c:1268-1282 semantics). External floors only
+  // rise; reset them before every independent search.
+  void local_floors(float out[kNumHarmonicLevels]) const;
+  void raise_external_floors(const float f[kNumHarmonicLevels]);
+  void reset_external_floors();
 
  private:
   struct Impl;

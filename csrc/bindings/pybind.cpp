@@ -509,6 +509,8 @@ PYBIND11_MODULE(_brp, m) {
         d["templates"] = s.templates;
         d["batches"] = s.batches;
         d["overflow_reruns"] = s.overflow_reruns;
+        d["select_batches"] = s.select_batches;
+        d["list_dma_copies"] = s.list_dma_copies;
         d["shared_series_batches"] = s.shared_series_batches;
         d["peer_series_copies"] = s.peer_series_copies;
         return d;
@@ -557,6 +559,9 @@ PYBIND11_MODULE(_brp, m) {
         d["t_total"] = res.t_total;
         d["gpu_ms"] = res.stats.gpu_ms;
         d["whiten_ms"] = res.stats.whiten_ms;
+        d["overflow_reruns"] = res.stats.overflow_reruns;
+        d["select_batches"] = res.stats.select_batches;
+        d["select_exits"] = res.stats.select_exits;
         return d;
       },
       py::arg("options"), py::arg("begin") = 0, py::arg("end") = 0, py::arg("write_output") = true,
@@ -599,6 +604,18 @@ PYBIND11_MODULE(_brp, m) {
           py::arg("begin"), py::arg("end"), py::arg("table") = CandidateTable())
       .def("geometry", [](SearchSession& s) { return geometry_to_dict(s.geometry()); })
       .def("total", &SearchSession::total)
+      .def("local_floors",
+           [](const SearchSession& s) {
+             float f[kNumHarmonicLevels];
+             s.local_floors(f);
+             return std::vector<float>(f, f + kNumHarmonicLevels);
+           })
+      .def("raise_external_floors",
+           [](SearchSession& s, std::vector<float> f) {
+             if (f.size() != static_cast<size_t>(kNumHarmonicLevels)) throw std::runtime_error("need 5 floors");
+             s.raise_external_floors(f.data());
+           })
+      .def("reset_external_floors", &SearchSession::reset_external_floors)
       .def("stats", [](SearchSession& s) {
         const BackendStats st = s.stats();
         py::dict d;
@@ -607,6 +624,9 @@ PYBIND11_MODULE(_brp, m) {
         d["templates"] = st.templates;
         d["batches"] = st.batches;
         d["overflow_reruns"] = st.overflow_reruns;
+        d["select_batches"] = st.select_batches;
+        d["select_exits"] = st.select_exits;
+        d["list_dma_copies"] = st.list_dma_copies;
         d["shared_series_batches"] = st.shared_series_batches;
         d["peer_series_copies"] = st.peer_series_copies;
         return d;

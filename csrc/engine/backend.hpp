@@ -29,7 +29,10 @@ struct BackendStats {
   double whiten_ms = 0;      // device time of the whitening step
   uint64_t templates = 0;
   uint64_t batches = 0;
-  uint64_t overflow_reruns = 0;
+  uint64_t overflow_reruns = 0;   // batches re-run with the bounded output after a list overflow
+  uint64_t select_batches = 0;    // batches that ran with the bounded output
+  uint64_t select_exits = 0;      // returns to the compacting path (floors rose)
+  uint64_t list_dma_copies = 0;   // long candidate lists DMA-copied instead of read in place
   uint64_t shared_series_batches = 0;  // batches that read another pipeline's series in place
   uint64_t peer_series_copies = 0;     // series taken device to device (peer / D2D), not from the host
 };

@@ -317,7 +317,25 @@ struct HipEngine::Impl {
   hipEvent_t prev_done = nullptr;  // completion event of the last completed batch (device-time statistics)
   uint32_t key_base = 0;        // template index of the current launch group within its batch
   bool group_reset = true;      // the current launch group zeroes the batch's candidate counter
-  uint32_t cap = 1u << 20;      // candidate slots per batch (all templates and levels)
+  uint32_t cap = 1u << 20;      // candidate slots per batch (all templates and levels; BRP_HS_CAP)
+  uint32_t bin_bits = 23;       // candidate key layout (hs_pack) of the geometry
+  // Bounded output (hipk::launch_harmonic_sum_select): per template and level
+  // only the values >= the 100th largest are emitted. Switched on when a
+  // batch's list overflows (that batch is re-run), off again once a batch's
+  // above-threshold count would fit the list comfortably. BRP_HS_SELECT=1: always.
+  bool select_mode = false;
+  bool select_forced = false;
+  DevBuf<float> sel_dense;
+  DevBuf<uint32_t> sel_hist, sel_state;
+  uint32_t dense_stride = 0;
+  int ensure_select() {
+    const size_t rows = static_cast<size_t>(batch) * 5;
+    int rc;
+    if (sel_dense.n < rows * dense_stride && (rc = sel_dense.alloc(rows * dense_stride))) return rc;
+    if (sel_hist.n < rows * hipk::kHsSelBins && (rc = sel_hist.alloc(rows * hipk::kHsSelBins))) return rc;
+    if (sel_state.n < rows * 4 && (rc = sel_state.alloc(rows * 4))) return rc;
+    return 0;
+  }
   uint32_t kcopy = 1024;        // slots copied back with every batch (more: second copy)
   // results in place (fg_out): longer lists are DMA-copied instead of read over
   // the PCIe BAR (uncached host reads; config 4 measured 12.8k vs 17.4k pairs/s
@@ -402,6 +420,7 @@ struct HipEngine::Impl {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;  // ev0: stage benchmark only; ev1: the batch's completion
     int nb = 0;
     bool pending = false;
+    bool sel = false;  // submitted with the bounded output (select_mode)
   };
   static constexpr int kIoSlots = 3;  // I/O slots; BRP_INFLIGHT picks how many are used (default 2)
   BatchIO io[kIoSlots];
@@ -693,6 +712,16 @@ struct HipEngine::Impl {
         ah.pyr = pyr.p;
         ah.pyr_stride = hipk::hs_pyr_stride(ps_stride);
         ah.key_base = key_base;
+        ah.bin_bits = bin_bits;
+        if (select_mode) {
+          hipk::HsSelectArgs sa{};
+          sa.dense = sel_dense.p;
+          sa.dense_stride = dense_stride;
+          sa.hist = sel_hist.p;
+          sa.state = sel_state.p;
+          sa.k = kCandPerLevel;
+          return hipk::launch_harmonic_sum_select(ah, sa, nb, stream);
+        }
         return hipk::launch_harmonic_sum(ah, nb, stream);
       }
       case kEpilogue:
@@ -712,6 +741,8 @@ struct HipEngine::Impl {
     TemplateDev* const tmpl0 = tmpl.p;
     float* const thr0 = thr.p;
     hipError_t e = enqueue_stage(kPrologue, nb);
+    // bounded output: list[0].y counts the batch's above-threshold values
+    if (e == hipSuccess && select_mode) e = hipMemsetAsync(cands.p, 0, sizeof(uint2), stream);
     for (int g0 = 0; e == hipSuccess && g0 < nb; g0 += batch) {
       const int ng = std::min(batch, nb - g0);
       tmpl.p = tmpl0 + g0;
@@ -957,7 +988,30 @@ int HipEngine::setup_impl(const SearchGeometry& g, const float* host_series, con
   d.ps_stride = std::max<uint32_t>((std::max(limit, g.fundamental_idx_hi) + 63) / 64 * 64, 64);
   // first harmonic-sum tile: i_start == 8 mod 16 and <= window_2 (-8 below 8)
   d.i_start = (g.window_2 >= 8) ? static_cast<int32_t>(((g.window_2 - 8) / 16) * 16 + 8) : -8;
+  // candidate keys sized to the geometry: bins < 2^bin_bits, and at most the
+  // templates per submitted batch the remaining key bits address
+  d.bin_bits = hipk::hs_bin_bits(std::max<uint32_t>(g.fundamental_idx_hi, 2));
+  const uint32_t key_templates = hipk::hs_key_templates(d.bin_bits);
+  if (key_templates == 0) {
+    log_message(LOG_ERROR, true, "fundamental_idx_hi %u: more bins than a candidate key addresses (2^%u).\n",
+                g.fundamental_idx_hi, hipk::kHsMaxBinBits);
+    return RADPUL_EVAL;
+  }
+  while (static_cast<uint32_t>(d.slot_cap()) > key_templates) {
+    if (d.serial > 1) d.serial = std::max(1, static_cast<int>(key_templates) / d.batch);
+    else d.batch = static_cast<int>(key_templates);
+  }
+  d.dense_stride = std::max<uint32_t>((g.fundamental_idx_hi + 63) / 64 * 64, 64);
+  if (const char* e = std::getenv("BRP_HS_CAP")) {
+    d.cap = std::max<uint32_t>(64u, static_cast<uint32_t>(std::atol(e)));
+    d.kcopy = std::min(d.kcopy, d.cap);
+    d.inplace_max = std::min(d.inplace_max, d.kcopy);
+  }
+  d.select_forced = std::getenv("BRP_HS_SELECT") != nullptr && std::atoi(std::getenv("BRP_HS_SELECT")) != 0;
+  d.select_mode = d.select_forced;
+  d.sel_dense.release();
   int rc;
+  if (d.select_mode && (rc = d.ensure_select())) return rc;
   const size_t B = static_cast<size_t>(d.batch);
   if ((rc = d.series.alloc(static_cast<size_t>(d.slots) * g.n_unpadded))) return rc;
   if ((rc = d.buf.alloc(B * d.plan.M))) return rc;
@@ -980,11 +1034,6 @@ int HipEngine::setup_impl(const SearchGeometry& g, const float* host_series, con
     d.bs_h.release();
   }
   if ((rc = d.delta.alloc(B))) return rc;
-  if (static_cast<size_t>(d.slot_cap()) > hipk::kHsMaxBatch || g.fundamental_idx_hi >= (1u << hipk::kHsBinBits)) {
-    log_message(LOG_ERROR, true, "Batch %zu / fundamental_idx_hi %u beyond the candidate key packing.\n", B,
-                g.fundamental_idx_hi);
-    return RADPUL_EVAL;
-  }
   const size_t BS = static_cast<size_t>(d.slot_cap());  // templates per I/O slot
   d.thr_bytes = (BS * hipk::kHsThrStride * sizeof(float) + 63) / 64 * 64;
   const size_t in_bytes = d.thr_bytes + sizeof(TemplateDev) * BS;
@@ -1385,6 +1434,7 @@ int HipEngine::submit(const TemplateInput* t, int nb, const float* thr, int thr_
   BRP_HIP_CHECK(hipEventRecord(d.ev1, d.stream), RADPUL_HIP_KERNEL_INVOKE);
   d.io[slot].nb = nb;
   d.io[slot].pending = true;
+  d.io[slot].sel = d.select_mode;
   d.io_next = (slot + 1) % Impl::kIoSlots;
   return 0;
 }
@@ -1412,11 +1462,42 @@ int HipEngine::complete(std::vector<TemplateCands>& out) {
   d.st.batches += 1;
   if (d.shared_series != nullptr) d.st.shared_series_batches += 1;
   d.st.templates += nb;
-  const uint32_t cnt = o.h_cands_p[0].x;
+  uint32_t cnt = o.h_cands_p[0].x;
+  bool ran_select = o.sel;
+  if (cnt > d.cap && !o.sel) {
+    // More above-threshold values than list slots (e.g. no -W: raw powers
+    // exceed the chi^2 thresholds almost everywhere). Re-run this batch with
+    // the bounded output (its parameters are still in the slot; the stream
+    // orders the re-run after any batch queued behind this one) and keep that
+    // mode for the following batches.
+    log_message(LOG_DEBUG, true, "Candidate list overflow (%u > %u slots, %d templates): bounded output.\n", cnt,
+                d.cap, nb);
+    int rc;
+    if ((rc = d.ensure_select())) return rc;
+    d.select_mode = true;
+    for (auto& kv : d.graphs) (void)hipGraphExecDestroy(kv.second);  // captured the compacting path
+    d.graphs.clear();
+    d.select_io(slot);
+    if (d.fg_in) std::atomic_thread_fence(std::memory_order_seq_cst);
+    BRP_HIP_CHECK(d.enqueue(nb), RADPUL_HIP_KERNEL_INVOKE);
+    BRP_HIP_CHECK(hipEventRecord(o.ev1, d.stream), RADPUL_HIP_KERNEL_INVOKE);
+    BRP_HIP_CHECK(hipEventSynchronize(o.ev1), RADPUL_HIP_KERNEL_INVOKE);
+    d.st.overflow_reruns += 1;
+    ran_select = true;
+    cnt = o.h_cands_p[0].x;
+    d.prev_done = nullptr;  // the statistics chain restarts
+  }
   if (cnt > d.cap) {
+    // bounded output overflowing: > cap / 5 equal values at one 100th place
     log_message(LOG_ERROR, true, "Candidate overflow (%u > %u slots) in a batch of %d templates.\n", cnt, d.cap, nb);
     return RADPUL_HIP_CAND_OVERFLOW;
   }
+  if (ran_select && d.select_mode && !d.select_forced && o.h_cands_p[0].y <= d.cap / 4) {
+    // the thresholds (table floors) rose: the compacting path fits again
+    d.select_mode = false;
+    d.st.select_exits += 1;
+  }
+  if (ran_select) d.st.select_batches += 1;
   const uint2* src = o.h_cands_p + 1;
   std::vector<uint2> extra;
   // beyond kcopy entries a DMA copy of the list beats reading it in place
@@ -1430,17 +1511,19 @@ int HipEngine::complete(std::vector<TemplateCands>& out) {
                   RADPUL_HIP_MEM_COPY_DEVICE_HOST);
     BRP_HIP_CHECK(hipStreamSynchronize(d.stream), RADPUL_HIP_MEM_COPY_DEVICE_HOST);
     src = extra.data();
-    d.st.overflow_reruns += 1;
+    d.st.list_dma_copies += 1;
   }
   out.clear();
   out.resize(nb);
-  constexpr uint32_t kBinMask = (1u << hipk::kHsBinBits) - 1u;
+  const uint32_t bb = d.bin_bits;
+  const uint32_t bin_mask = static_cast<uint32_t>((1ull << bb) - 1u);
   for (uint32_t q = 0; q < cnt; ++q) {
     const uint32_t key = src[q].x;
-    const uint32_t k = key >> 26, h = (key >> hipk::kHsBinBits) & 7u;
+    const uint32_t k = static_cast<uint32_t>(static_cast<uint64_t>(key) >> (bb + 3)), h = (key >> bb) & 7u;
+    if (k >= static_cast<uint32_t>(nb) || h >= static_cast<uint32_t>(kNumHarmonicLevels)) return RADPUL_EVAL;
     float p;
     std::memcpy(&p, &src[q].y, sizeof(float));
-    out[k].level[h].push_back(BinPower{key & kBinMask, p});
+    out[k].level[h].push_back(BinPower{key & bin_mask, p});
   }
   for (int k = 0; k < nb; ++k)
     for (int h = 0; h < kNumHarmonicLevels; ++h) {

@@ -54,7 +54,11 @@ __device__ __forceinline__ void emit(uint32_t* counter, uint2* list, uint32_t ca
 // (Measured alternatives -- LDS-staged runs, XCD-contiguous tiles, 4 or 16
 // indices per lane, an MFMA selection-matrix sum -- are kept out of the
 // product in tools/experiments/hs_variants.hip; profiles/hs_variants_r2.txt.)
-template <int MODE>
+//
+// DENSE (the bounded-output path, launch_harmonic_sum_select): instead of
+// emitting, every level value of [w2, fhi) is written to a.dense (0 where it
+// does not exceed its threshold).
+template <int MODE, bool DENSE = false>
 __global__ void __launch_bounds__(kThreads) harmonic_sum_kernel(HSArgs a) {
 #pragma clang fp contract(off)
   constexpr int TILE = kHsTile;
@@ -138,7 +142,11 @@ __global__ void __launch_bounds__(kThreads) harmonic_sum_kernel(HSArgs a) {
     const int i = i0 + t;
     const bool in = t < TILE && (i >= w2 && i < fhi);
     const float p = in ? p0[it] : 0.0f;
-    emit(count, list, a.cap, in && p > thr0, hs_pack(a.key_base + b, 0, static_cast<uint32_t>(i)), p);
+    if constexpr (DENSE) {
+      if (in) a.dense[(static_cast<size_t>(b) * 5 + 0) * a.dense_stride + i] = p > thr0 ? p : 0.0f;
+    } else {
+      emit(count, list, a.cap, in && p > thr0, hs_pack(a.key_base + b, 0, static_cast<uint32_t>(i), a.bin_bits), p);
+    }
   }
   // levels 1..4: group of 2^h consecutive i starting at s == 2^(h-1) mod 2^h;
   // one thread per group, stride-2^h reads made (nearly) conflict free by the
@@ -151,20 +159,25 @@ __global__ void __launch_bounds__(kThreads) harmonic_sum_kernel(HSArgs a) {
     const int first = static_cast<int>((off - (i0 % g) + g) % g);
     const int ngroups = (TILE - first + g - 1) / g;
     for (int q = threadIdx.x; q < ((ngroups + kThreads - 1) / kThreads) * kThreads; q += kThreads) {
-      bool pred = false;
+      bool pred = false, inr = false;
       int j = 0;
       float m = ninf;
       if (q < ngroups) {
         const int t0 = first + q * g;
         j = (i0 + t0 + off) >> h;  // arithmetic shift: negative groups stay below w2
         if (j >= w2 && j < fhi) {
+          inr = true;
 #pragma unroll
           for (int u = 0; u < 16; ++u)
             if (u < g) m = fmaxf(m, sv[h - 1][sidx(t0 + u)]);
           pred = m > thr;
         }
       }
-      emit(count, list, a.cap, pred, hs_pack(a.key_base + b, h, static_cast<uint32_t>(j)), m);
+      if constexpr (DENSE) {
+        if (inr) a.dense[(static_cast<size_t>(b) * 5 + h) * a.dense_stride + j] = pred ? m : 0.0f;
+      } else {
+        emit(count, list, a.cap, pred, hs_pack(a.key_base + b, h, static_cast<uint32_t>(j), a.bin_bits), m);
+      }
     }
   }
 }
@@ -669,7 +682,7 @@ __global__ void __launch_bounds__(256) hs_pruned_kernel(HSArgs a, uint32_t nblk)
     wave_sync();
     // level 0: the spectrum itself, indices of the block
     const bool in0 = act && li < kBlk && i >= w2 && i < fhi;
-    emit(count, list, a.cap, in0 && p0 > thr[0], hs_pack(a.key_base + b, 0, static_cast<uint32_t>(i)), p0);
+    emit(count, list, a.cap, in0 && p0 > thr[0], hs_pack(a.key_base + b, 0, static_cast<uint32_t>(i), a.bin_bits), p0);
     // levels 1..4: lane li < 15 owns one group (8 of level 1, 4 of level 2, 2 of level 3, 1 of level 4)
     int h = 4, t0 = 0;
     if (li < 8) { h = 1; t0 = 2 * li + 1; }
@@ -684,8 +697,126 @@ __global__ void __launch_bounds__(256) hs_pruned_kernel(HSArgs a, uint32_t nblk)
       j = (ib + t0 + (g >> 1)) >> h;
       pred = j >= w2 && j < fhi && m > thr[h];
     }
-    emit(count, list, a.cap, pred, hs_pack(a.key_base + b, static_cast<uint32_t>(h), static_cast<uint32_t>(j)), m);
+    emit(count, list, a.cap, pred,
+         hs_pack(a.key_base + b, static_cast<uint32_t>(h), static_cast<uint32_t>(j), a.bin_bits), m);
     wave_sync();
+  }
+}
+
+
+// ------------------------------------------------------------ bounded output
+// Radix select of the K-th largest level value per (template, level) over
+// the dense values of [w2, fhi): three rounds of 11 / 11 / 10 bits of the
+// float bit pattern (positive floats order like their bits), each a histogram
+// of the values matching the prefix found so far, then one wave picking the
+// next digit. State per (template, level): prefix, K remaining, "fewer than K
+// values above threshold" flag, number of such values.
+constexpr int kSelShift[3] = {21, 10, 0};
+constexpr int kSelBits[3] = {11, 11, 10};
+constexpr uint32_t kSelChunk = 256 * 16;  // values per histogram workgroup
+
+template <int ROUND>
+__global__ void __launch_bounds__(256) hs_sel_hist_kernel(HSArgs a, HsSelectArgs s) {
+  constexpr int kShift = kSelShift[ROUND], kBits = kSelBits[ROUND];
+  __shared__ uint32_t hist[kHsSelBins];
+  const uint32_t h = blockIdx.y, b = blockIdx.z;
+  const size_t row = static_cast<size_t>(b) * 5 + h;
+  const uint32_t* st = s.state + row * 4;
+  if (ROUND > 0 && st[2] != 0) return;  // uniform: fewer than K values, nothing to refine
+  for (uint32_t e = threadIdx.x; e < (1u << kBits); e += 256) hist[e] = 0;
+  __syncthreads();
+  const uint32_t prefix = st[0];
+  const uint32_t* v = reinterpret_cast<const uint32_t*>(s.dense) + row * s.dense_stride;
+  const uint32_t lo = a.w2 + blockIdx.x * kSelChunk, hi = min(lo + kSelChunk, a.fhi);
+  for (uint32_t j = lo + threadIdx.x; j < hi; j += 256) {
+    const uint32_t u = v[j];
+    if (u == 0 || (u >> 31) != 0) continue;  // not above threshold
+    if (ROUND > 0 && (u >> (kShift + kBits)) != (prefix >> (kShift + kBits))) continue;
+    atomicAdd(&hist[(u >> kShift) & ((1u << kBits) - 1u)], 1u);
+  }
+  __syncthreads();
+  uint32_t* g = s.hist + row * kHsSelBins;
+  for (uint32_t e = threadIdx.x; e < (1u << kBits); e += 256)
+    if (hist[e] != 0) atomicAdd(&g[e], hist[e]);
+}
+
+// one wave per (template, level): lane l owns bins [32 l, 32 l + 32)
+template <int ROUND>
+__global__ void __launch_bounds__(64) hs_sel_pick_kernel(HSArgs a, HsSelectArgs s) {
+  constexpr int kShift = kSelShift[ROUND], kBits = kSelBits[ROUND];
+  constexpr int kPer = (1 << kBits) / kWave;
+  const uint32_t h = blockIdx.x, b = blockIdx.y;
+  const size_t row = static_cast<size_t>(b) * 5 + h;
+  uint32_t* st = s.state + row * 4;
+  uint32_t* g = s.hist + row * kHsSelBins;
+  const int lane = threadIdx.x;
+  if (ROUND > 0 && st[2] != 0) return;
+  uint32_t mine[kPer];
+  uint32_t sum = 0;
+#pragma unroll
+  for (int e = 0; e < kPer; ++e) {
+    mine[e] = g[lane * kPer + e];
+    g[lane * kPer + e] = 0;  // cleared for the next round
+    sum += mine[e];
+  }
+  // suffix sums over the lanes: values in the bins of lanes >= lane
+  uint32_t suf = sum;
+#pragma unroll
+  for (int off = 1; off < kWave; off <<= 1) {
+    const uint32_t o = __shfl_down(suf, off, kWave);
+    if (lane + off < kWave) suf += o;
+  }
+  const uint32_t krem = st[1];
+  const uint32_t total = __shfl(suf, 0, kWave);
+  if (ROUND == 0) {
+    if (lane == 0) {
+      st[3] = total;
+      atomicAdd(&a.list[0].y, total);
+    }
+    if (total < krem) {  // fewer than K values above threshold: all of them are kept
+      if (lane == 0) st[2] = 1;
+      return;
+    }
+  }
+  // the highest lane whose suffix still reaches krem holds the K-th value's digit
+  const unsigned long long reach = __ballot(suf >= krem);
+  const int L = 63 - __clzll(static_cast<long long>(reach));
+  if (lane == L) {
+    uint32_t above = suf - sum;  // values in higher lanes' bins
+    int digit = 0;
+    for (int e = kPer - 1; e >= 0; --e) {
+      if (above + mine[e] >= krem) {
+        digit = lane * kPer + e;
+        break;
+      }
+      above += mine[e];
+    }
+    st[0] |= static_cast<uint32_t>(digit) << kShift;
+    st[1] = krem - above;
+  }
+}
+
+__global__ void hs_sel_init_kernel(uint32_t* state, uint32_t rows, uint32_t k) {
+  const uint32_t r = blockIdx.x * 256u + threadIdx.x;
+  if (r < rows) reinterpret_cast<uint4*>(state)[r] = make_uint4(0u, k, 0u, 0u);
+}
+
+// emit every value >= the K-th largest (all of them when there are fewer than K)
+__global__ void __launch_bounds__(256) hs_sel_emit_kernel(HSArgs a, HsSelectArgs s) {
+  const uint32_t h = blockIdx.y, b = blockIdx.z;
+  const size_t row = static_cast<size_t>(b) * 5 + h;
+  const uint32_t* st = s.state + row * 4;
+  const uint32_t kth = st[2] != 0 ? 1u : st[0];
+  const uint32_t* v = reinterpret_cast<const uint32_t*>(s.dense) + row * s.dense_stride;
+  const uint32_t lo = a.w2 + blockIdx.x * kSelChunk, hi = min(lo + kSelChunk, a.fhi);
+  uint32_t* count = &a.list[0].x;
+  uint2* list = a.list + 1;
+  // whole-wave iterations (emit aggregates with a ballot)
+  for (uint32_t j0 = lo; j0 < hi; j0 += 256) {
+    const uint32_t j = j0 + threadIdx.x;
+    const uint32_t u = j < hi ? v[j] : 0u;
+    const bool keep = u != 0 && (u >> 31) == 0 && u >= kth;
+    emit(count, list, a.cap, keep, hs_pack(a.key_base + b, h, j, a.bin_bits), __uint_as_float(u));
   }
 }
 
@@ -732,6 +863,33 @@ hipError_t launch_harmonic_sum(const HSArgs& a, int batch, hipStream_t s) {
     case HS_F16: hipLaunchKernelGGL(harmonic_sum_kernel<HS_F16>, grid, dim3(kThreads), 0, s, a); break;
     default: hipLaunchKernelGGL(harmonic_sum_kernel<HS_F32>, grid, dim3(kThreads), 0, s, a); break;
   }
+  return hipGetLastError();
+}
+
+
+hipError_t launch_harmonic_sum_select(const HSArgs& a0, const HsSelectArgs& s, int batch, hipStream_t st) {
+  HSArgs a = a0;
+  a.dense = s.dense;
+  a.dense_stride = s.dense_stride;
+  const uint32_t tiles = hs_num_tiles(a.i_start, a.hhi);
+  if (a.fhi <= a.w2 || tiles == 0 || s.dense_stride < a.fhi) return hipSuccess;
+  hipError_t e;
+  const size_t rows = static_cast<size_t>(batch) * 5;
+  if ((e = hipMemsetAsync(s.dense, 0, rows * s.dense_stride * sizeof(float), st)) != hipSuccess) return e;
+  if ((e = hipMemsetAsync(s.hist, 0, rows * kHsSelBins * sizeof(uint32_t), st)) != hipSuccess) return e;
+  const dim3 grid(tiles, batch);
+  if (a.mode == HS_F16) hipLaunchKernelGGL((harmonic_sum_kernel<HS_F16, true>), grid, dim3(kThreads), 0, st, a);
+  else hipLaunchKernelGGL((harmonic_sum_kernel<HS_F32, true>), grid, dim3(kThreads), 0, st, a);
+  const dim3 gh((a.fhi - a.w2 + kSelChunk - 1) / kSelChunk, 5, batch), gp(5, batch);
+  hipLaunchKernelGGL(hs_sel_init_kernel, dim3((rows + 255) / 256), dim3(256), 0, st, s.state,
+                     static_cast<uint32_t>(rows), s.k);
+  hipLaunchKernelGGL(hs_sel_hist_kernel<0>, gh, dim3(256), 0, st, a, s);
+  hipLaunchKernelGGL(hs_sel_pick_kernel<0>, gp, dim3(64), 0, st, a, s);
+  hipLaunchKernelGGL(hs_sel_hist_kernel<1>, gh, dim3(256), 0, st, a, s);
+  hipLaunchKernelGGL(hs_sel_pick_kernel<1>, gp, dim3(64), 0, st, a, s);
+  hipLaunchKernelGGL(hs_sel_hist_kernel<2>, gh, dim3(256), 0, st, a, s);
+  hipLaunchKernelGGL(hs_sel_pick_kernel<2>, gp, dim3(64), 0, st, a, s);
+  hipLaunchKernelGGL(hs_sel_emit_kernel, gh, dim3(256), 0, st, a, s);
   return hipGetLastError();
 }
 

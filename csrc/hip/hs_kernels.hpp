@@ -38,6 +38,9 @@ struct HSArgs {
   float* pyr;
   uint32_t pyr_stride;
   uint32_t key_base;  // index of template 0 of this launch within the batch's candidate list
+  uint32_t bin_bits;  // candidate key layout (hs_pack): bins < 2^bin_bits
+  float* dense;       // select path: [batch][5][dense_stride] level values (HsSelectArgs)
+  uint32_t dense_stride;
 };
 
 // cells covering the spectrum row, room for 4-bin cells (bins >= hhi count as 0)
@@ -46,14 +49,51 @@ __host__ __device__ constexpr uint32_t hs_pyr_stride(uint32_t ps_stride) { retur
 uint32_t hs_num_blocks(int32_t i_start, uint32_t hhi);
 
 constexpr uint32_t kHsThrStride = 8;  // floats per template in the threshold array (5 used)
-constexpr uint32_t kHsBinBits = 23;  // bins < 2^23, levels < 8, templates per batch < 64
-constexpr uint32_t kHsMaxBatch = 64;
-__host__ __device__ constexpr uint32_t hs_pack(uint32_t k, uint32_t h, uint32_t bin) {
-  return (k << 26) | (h << kHsBinBits) | bin;
+constexpr uint32_t kHsMaxBatch = 64;  // templates per submitted batch (threshold / parameter area)
+// Candidate key: template index in the batch | level (3 bits) | bin (bin_bits),
+// with bin_bits sized to the geometry's fundamental_idx_hi (hs_bin_bits), so any
+// -f / -P the reference accepts fits (fundamental_idx_hi <= fft_size ~ 2.1e7 on a
+// 2^22-sample WU at -P 10: 25 bits, 4 template bits). Beyond 2^29 bins no key fits.
+constexpr uint32_t kHsMaxBinBits = 29;
+__host__ __device__ constexpr uint32_t hs_pack(uint32_t k, uint32_t h, uint32_t bin, uint32_t bin_bits) {
+  return static_cast<uint32_t>(static_cast<uint64_t>(k) << (bin_bits + 3)) | (h << bin_bits) | bin;
+}
+inline uint32_t hs_bin_bits(uint32_t fhi) {
+  uint32_t b = 1;
+  while (b < 32 && (1ull << b) < fhi) ++b;  // every bin < fhi <= 2^b
+  return b;
+}
+// templates a batch's keys can address (0: the geometry has no key layout)
+inline uint32_t hs_key_templates(uint32_t bin_bits) {
+  if (bin_bits > kHsMaxBinBits) return 0;
+  const uint64_t n = 1ull << (32 - 3 - bin_bits);
+  return static_cast<uint32_t>(n < kHsMaxBatch ? n : kHsMaxBatch);
 }
 
 uint32_t hs_num_tiles(int32_t i_start, uint32_t hhi);
 hipError_t launch_harmonic_sum(const HSArgs& a, int batch, hipStream_t s);
+
+// ---- bounded candidate output (the overflow path)
+// For every template and level, a bin whose level value has >= K values of
+// the same template and level strictly above it can never enter the K-entry
+// table level (its K betters are distinct bins that the
+// table then holds at >= their powers), so emitting only the values >= the
+// K-th largest (ties kept) gives the in-order applier exactly the table of
+// the full list. Used when a batch's list overflows (no -W: raw powers put
+// nearly every bin above the chi^2 thresholds): the level values are written
+// densely, the K-th largest found by a 3-round radix select on their bits
+// (positive floats order like their bit patterns), and only those emitted.
+struct HsSelectArgs {
+  float* dense;           // [batch][5][dense_stride]: level value if > threshold, else 0
+  uint32_t dense_stride;  // >= fhi
+  uint32_t* hist;         // [batch][5][kHsSelBins] radix histograms
+  uint32_t* state;        // [batch][5][4]: prefix, k remaining, fewer-than-K flag, positives
+  uint32_t k;             // values kept per template and level (kCandPerLevel)
+};
+constexpr uint32_t kHsSelBins = 2048;
+// list[0].y accumulates the number of values above threshold of the batch
+// (what the compacting path would have emitted; the engine's mode switch)
+hipError_t launch_harmonic_sum_select(const HSArgs& a, const HsSelectArgs& s, int batch, hipStream_t st);
 
 }  // namespace hipk
 }  // namespace brp

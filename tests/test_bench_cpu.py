@@ -42,6 +42,41 @@ def test_bench_multirank_cpu_rehearsal(nproc, tmp_path):
     assert (tmp_path / "one.cand").read_text() == (tmp_path / "many.cand").read_text()
 
 
+def _bench_direct(nproc, tmp, out, extra=()):
+    """bench.py started WITHOUT a launcher: it must start the ranks itself."""
+    cmd = [sys.executable, "bench.py", "--gpus", str(nproc), "--steps", "1", "--warmup", "1", "--cpu", "--batch", "3",
+           "--write-output", str(out), *extra]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(TMPDIR=str(tmp), OMP_NUM_THREADS="1", BRP_NO_RESULT_HEADER="1")
+    return subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+
+
+def test_bench_gpus_without_launcher_starts_the_ranks(tmp_path):
+    """`bench.py --gpus 2` with no torchrun: two rank processes, n_gpus 2 in the
+    JSON line, the result file equal to the one-rank run byte for byte."""
+    one = _bench(1, tmp_path / "w1", tmp_path / "one.cand")
+    r = _bench_direct(2, tmp_path / "w2", tmp_path / "two.cand")
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["launched_by"] == "bench.py", rec
+    assert rec["floor_sync_rounds_last_step"] >= 1, rec
+    assert one["n_gpus"] == 1
+    assert (tmp_path / "one.cand").read_text() == (tmp_path / "two.cand").read_text()
+
+
+def test_bench_world_size_mismatch_is_an_error(tmp_path):
+    """A launcher that starts fewer ranks than --gpus asks for is refused
+    (the JSON line would otherwise claim a different GPU count)."""
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", TMPDIR=str(tmp_path))
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "1", "--warmup", "0", "--cpu"], cwd=ROOT,
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert "WORLD_SIZE=1" in r.stderr
+
+
 def test_collective_timeout_degrades_to_single_gpu(tmp_path):
     """BRP_FAULT=collective_timeout:1 stalls rank 1 before the all-gather; rank 0
     times out, aborts the process group, searches the missing shard itself and

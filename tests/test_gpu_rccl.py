@@ -39,6 +39,26 @@ def _worker(rank, world, port, opts, out_dir):
         dist.destroy_process_group()
 
 
+def test_bench_refuses_more_gpus_than_visible(gpu, tmp_path):
+    """`bench.py --gpus N` without a launcher starts N ranks itself; asking for
+    more GPUs than the box has exits non-zero before any GPU work, with no JSON
+    line (it never reports a 1-GPU number as N GPUs)."""
+    import subprocess
+    import sys
+
+    import torch
+
+    from conftest import ROOT
+
+    n = torch.cuda.device_count() + 1
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", str(n), "--steps", "1", "--warmup", "0"], cwd=ROOT,
+                       env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert "device(s) are visible" in r.stderr, r.stderr[-2000:]
+
+
 def test_rccl_two_ranks_equal_single(brp, gpu, tmp_path):
     import torch
 

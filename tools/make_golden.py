@@ -10,7 +10,11 @@ benchmark flags (-A 0.08 -P 3.0 -f 400.0 -W). Output (tracked in git):
 The reference's smoke target (debian/patches/benchmark.patch: first 200
 templates at -A 0.04 -P 3.0 -W -z, default -f 250) has its own golden files:
   python tools/make_golden.py --end 200 --fA 0.04 --f0 250   (suffix _first200_A0.04_f250)
-Usage: python tools/make_golden.py [--threads 8] [--end N] [--fA 0.08] [--f0 400]
+Reference-legal inputs outside the benchmark flags (the GPU's bounded-output
+and wide-key paths, tests/test_gpu_bounded.py):
+  python tools/make_golden.py --end 20 --no-white              (raw powers: every bin above chi^2)
+  python tools/make_golden.py --end 6 --padding 5 --f0 8000 --fA 0.9999   (fundamental_idx_hi > 2^23)
+Usage: python tools/make_golden.py [--threads 8] [--end N] [--fA 0.08] [--f0 400] [--padding 3] [--no-white]
 """
 from __future__ import annotations
 
@@ -31,6 +35,8 @@ def main() -> None:
     ap.add_argument("--end", type=int, default=0, help="templates [0, end) (0: whole bank)")
     ap.add_argument("--fA", type=float, default=0.08, help="false-alarm rate -A")
     ap.add_argument("--f0", type=float, default=400.0, help="maximum signal frequency -f")
+    ap.add_argument("--padding", type=float, default=3.0, help="padding factor -P")
+    ap.add_argument("--no-white", action="store_true", help="no whitening (no -W)")
     ap.add_argument("--out", default=str(ROOT / "data" / "golden"))
     a = ap.parse_args()
     os.environ["BRP_NO_RESULT_HEADER"] = "1"
@@ -42,19 +48,22 @@ def main() -> None:
     out = Path(a.out)
     out.mkdir(parents=True, exist_ok=True)
     suffix = (("" if a.end == 0 else f"_first{a.end}") + ("" if a.fA == 0.08 else f"_A{a.fA:g}") +
-              ("" if a.f0 == 400.0 else f"_f{a.f0:g}"))
+              ("" if a.f0 == 400.0 else f"_f{a.f0:g}") + ("" if a.padding == 3.0 else f"_P{a.padding:g}") +
+              ("_noW" if a.no_white else ""))
     cfg = SearchConfig.benchmark(str(D / "p2030.20151015.G187.41-00.88.N.b2s0g0.00000_1099.bin4"),
                                  str(D / "stochastic_full.bank"),
                                  str(D / "p2030.20151015.G187.41-00.88.N.b2s0g0.00000.zap"),
                                  outputfile=str(out / f"bench_wu_cpu_results{suffix}.txt"), batch=1, use_cpu=True)
     cfg.fA = a.fA
     cfg.f0 = a.f0
+    cfg.padding = a.padding
+    cfg.white = not a.no_white
     t0 = time.time()
     r = brp.run_search(cfg.options(), 0, a.end, True, False, a.threads)
     dt = time.time() - t0
     (out / f"bench_wu_cpu_table{suffix}.bin").write_bytes(bytes(r["table"].to_bytes()))
     meta = dict(templates=r["templates_run"], templates_total=r["templates_total"], seconds=dt, threads=a.threads,
-                flags=f"-A {a.fA:g} -P 3.0 -f {a.f0:g} -W", backend="cpu golden (double FFT, reference float order)")
+                flags=f"-A {a.fA:g} -P {a.padding:g} -f {a.f0:g}" + ("" if a.no_white else " -W"), backend="cpu golden (double FFT, reference float order)")
     (out / f"bench_wu_cpu_meta{suffix}.json").write_text(json.dumps(meta, indent=1) + "\n")
     print(json.dumps(meta))
 
