@@ -6,10 +6,11 @@ inserts, screensaver/progress, checkpoint timer, BOINC status) fed by
 An 8-GPU node at the measured ~19 k templates/s per MI355X needs the applier
 to sustain ~152 k templates/s with two synthetic candidates per level and
 template (the benchmark WU averages well under one once the table has
-filled). The 24 replay workers and the applier are 25 busy threads: on a
-host with at least 16 CPUs the test asserts the node rate; on smaller hosts
-(this 8-CPU build container measures 200-250 k alone and less under a
-parallel test run) it asserts half of it and reports the rate."""
+filled). The 24 replay workers and the applier are 25 busy threads; the
+8-CPU build container measures 240 k templates/s (best of the runs) even with
+an 8-thread CPU job beside it, so the full node rate is asserted there too.
+BRP_APPLIER_RATE_REPORT_ONLY=1 turns the assertion into a report for shared
+or heavily loaded CI hosts (wall-clock rates are not a correctness check)."""
 import os
 
 import numpy as np
@@ -39,7 +40,7 @@ def _rate(brp, big, per_level, monkeypatch):
     opts = dict(inputfile=big["wu"], templatebank=big["bank"], zaplistfile=big["zap"], outputfile=str(d / "o.cand"),
                 checkpointfile=str(d / "cp.cpt"), f0=400.0, padding=1.0, fA=0.08, window=50, white=True, batch=1)
     best = 0.0
-    for _ in range(3):
+    for _ in range(5):
         for f in ("o.cand", "cp.cpt"):
             if (d / f).exists():
                 os.remove(d / f)
@@ -52,8 +53,9 @@ def _rate(brp, big, per_level, monkeypatch):
 def test_applier_headroom_eight_gpus(brp, big, monkeypatch):
     rate = _rate(brp, big, 2, monkeypatch)
     print(f"applier: {rate:.0f} templates/s with 24 replay pipelines, 2 candidates per level")
-    need = NODE_RATE if (os.cpu_count() or 1) >= 16 else NODE_RATE // 2
-    assert rate >= need, (rate, need)
+    if os.environ.get("BRP_APPLIER_RATE_REPORT_ONLY"):
+        return
+    assert rate >= NODE_RATE, (rate, NODE_RATE)
 
 
 def test_replay_search_writes_a_complete_result(brp, big, monkeypatch):
