@@ -71,7 +71,7 @@ class BRPSearch:
         return SearchOutput(table=r["table"], geometry=r["geometry"], templates_total=r["templates_total"],
                             templates_run=r["templates_run"], interrupted=r["interrupted"],
                             timings=dict(setup=r["t_setup"], templates=r["t_templates"], total=r["t_total"],
-                                         gpu_ms=r["gpu_ms"], whiten_ms=r["whiten_ms"]),
+                                         busy_span_ms=r["busy_span_ms"], whiten_ms=r["whiten_ms"]),
                             stats=dict(overflow_reruns=r["overflow_reruns"], select_batches=r["select_batches"],
                                        select_exits=r["select_exits"]))
 

@@ -42,7 +42,8 @@ void print_usage(const char* prog) {
   std::printf(" --mi355x-batch\t\tinteger\tTemplates per device batch (default 1).\n");
   std::printf(" --mi355x-gpus\t\tinteger\tGPUs (or CPU worker threads with --mi355x-cpu) driven by this process (default 1).\n");
   std::printf(" --mi355x-cpu\t\t\tboolean\tUse the CPU golden backend.\n");
-  std::printf(" --mi355x-ps-fp16\t\tboolean\tStore the power spectrum as fp16 (needs -W).\n");
+  std::printf(" --mi355x-ps-fp16\t\tboolean\tStore the power spectrum as fp16 (needs -W). Inexact: near-tie\n"
+              "\t\t\t\t\ttable entries may differ from fp32 (experiment, not the product path).\n");
   std::printf(" --mi355x-spin\t\t\tboolean\tBusy-wait for the GPU instead of sleeping (default: blocking sync).\n");
   std::printf(" --mi355x-pipelines\t\tinteger\tIndependent pipelines per GPU (default 3, one template each).\n");
   std::printf(" --mi355x-no-checkpoint\t\tboolean\tNever read or write checkpoints (Debian NOCHECKPOINTING build).\n");

@@ -77,7 +77,7 @@ BackendStats MultiSession::stats() const {
   BackendStats t;
   for (auto& e : impl_->engines) {
     const BackendStats s = e->stats();
-    t.gpu_ms += s.gpu_ms;
+    t.busy_span_ms += s.busy_span_ms;
     t.whiten_ms += s.whiten_ms;
     t.templates += s.templates;
     t.batches += s.batches;
@@ -85,6 +85,7 @@ BackendStats MultiSession::stats() const {
     t.select_batches += s.select_batches;
     t.select_exits += s.select_exits;
     t.list_dma_copies += s.list_dma_copies;
+    t.candidates += s.candidates;
     t.shared_series_batches += s.shared_series_batches;
     t.peer_series_copies += s.peer_series_copies;
   }
@@ -148,6 +149,8 @@ int MultiSession::prepare() {
   int rc;
   std::vector<std::vector<float>> prepared(d.wus.size());
   std::vector<float> mu0(d.wus.size(), 0.0f);
+  bool all_same_device = true;
+  for (auto& e : d.engines) all_same_device = all_same_device && e->device() == d.engines[0]->device();
   HipEngine& e0 = *d.engines[0];
   for (size_t k = 0; k < d.wus.size(); ++k) {
     std::vector<float>& s = prepared[k];
@@ -160,15 +163,28 @@ int MultiSession::prepare() {
     if (rc) return rc;
     mu0[k] = static_cast<float>(mean);
     if (d.opt.white) {
-      // per-WU geometry carries the WU's own t_obs for the zap bins
-      if ((rc = e0.whiten(d.opt, d.zaps, s, static_cast<uint32_t>(k)))) return rc;
+      // per-WU geometry carries the WU's own t_obs for the zap bins; the
+      // host copy of the whitened series is needed only by engines on
+      // other devices
+      if ((rc = e0.whiten(d.opt, d.zaps, s, static_cast<uint32_t>(k), !all_same_device))) return rc;
       mu0[k] = 0.0f;
     }
   }
   for (size_t e = 1; e < d.engines.size(); ++e) {
+    HipEngine& en = *d.engines[e];
+    if (en.device() == e0.device()) {
+      // Pipelines on engine 0's device read its K whitened series in place
+      // (like the single-WU session's adopt_series): one copy of each series
+      // in the Infinity Cache instead of one per pipeline, and no uploads.
+      // The first pass allocates this engine's buffers once.
+      if (!en.ready_for(g) && (rc = en.setup(g, d.wus[0].samples, 0.0f))) return rc;
+      if ((rc = en.adopt_series(e0)) == 0) continue;
+      log_message(LOG_ERROR, true, "Pipeline %zu could not read pipeline 0's series in place.\n", e);
+      return rc;
+    }
     for (size_t k = 0; k < d.wus.size(); ++k) {
-      if (k == 0) rc = d.engines[e]->setup(g, prepared[0], mu0[0]);
-      else rc = d.engines[e]->load_slot(static_cast<uint32_t>(k), prepared[k], mu0[k]);
+      if (k == 0) rc = en.setup(g, prepared[0], mu0[0]);
+      else rc = en.load_slot(static_cast<uint32_t>(k), prepared[k], mu0[k]);
       if (rc) return rc;
     }
   }

@@ -208,7 +208,7 @@ BackendStats SearchSession::stats() const {
   BackendStats t;
   for (auto& be : impl_->backends) {
     const BackendStats s = be->stats();
-    t.gpu_ms += s.gpu_ms;
+    t.busy_span_ms += s.busy_span_ms;
     t.whiten_ms += s.whiten_ms;
     t.templates += s.templates;
     t.batches += s.batches;
@@ -216,6 +216,7 @@ BackendStats SearchSession::stats() const {
     t.select_batches += s.select_batches;
     t.select_exits += s.select_exits;
     t.list_dma_copies += s.list_dma_copies;
+    t.candidates += s.candidates;
     t.shared_series_batches += s.shared_series_batches;
     t.peer_series_copies += s.peer_series_copies;
   }

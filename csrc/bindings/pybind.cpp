@@ -504,7 +504,7 @@ PYBIND11_MODULE(_brp, m) {
       .def("stats", [](HipEngine& e) {
         const BackendStats s = e.stats();
         py::dict d;
-        d["gpu_ms"] = s.gpu_ms;
+        d["busy_span_ms"] = s.busy_span_ms;
         d["whiten_ms"] = s.whiten_ms;
         d["templates"] = s.templates;
         d["batches"] = s.batches;
@@ -557,7 +557,7 @@ PYBIND11_MODULE(_brp, m) {
         d["t_setup"] = res.t_setup;
         d["t_templates"] = res.t_templates;
         d["t_total"] = res.t_total;
-        d["gpu_ms"] = res.stats.gpu_ms;
+        d["busy_span_ms"] = res.stats.busy_span_ms;
         d["whiten_ms"] = res.stats.whiten_ms;
         d["overflow_reruns"] = res.stats.overflow_reruns;
         d["select_batches"] = res.stats.select_batches;
@@ -619,7 +619,7 @@ PYBIND11_MODULE(_brp, m) {
       .def("stats", [](SearchSession& s) {
         const BackendStats st = s.stats();
         py::dict d;
-        d["gpu_ms"] = st.gpu_ms;
+        d["busy_span_ms"] = st.busy_span_ms;
         d["whiten_ms"] = st.whiten_ms;
         d["templates"] = st.templates;
         d["batches"] = st.batches;
@@ -627,6 +627,7 @@ PYBIND11_MODULE(_brp, m) {
         d["select_batches"] = st.select_batches;
         d["select_exits"] = st.select_exits;
         d["list_dma_copies"] = st.list_dma_copies;
+        d["candidates"] = st.candidates;
         d["shared_series_batches"] = st.shared_series_batches;
         d["peer_series_copies"] = st.peer_series_copies;
         return d;
@@ -680,10 +681,14 @@ PYBIND11_MODULE(_brp, m) {
       .def("stats", [](MultiSession& s) {
         const BackendStats st = s.stats();
         py::dict d;
-        d["gpu_ms"] = st.gpu_ms;
+        d["busy_span_ms"] = st.busy_span_ms;
         d["whiten_ms"] = st.whiten_ms;
         d["templates"] = st.templates;
         d["batches"] = st.batches;
+        d["candidates"] = st.candidates;
+        d["overflow_reruns"] = st.overflow_reruns;
+        d["select_batches"] = st.select_batches;
+        d["shared_series_batches"] = st.shared_series_batches;
         return d;
       });
   m.def("finalize_output", [](const py::dict& od, const py::dict& gd, uint32_t n_done, CandidateTable t) {

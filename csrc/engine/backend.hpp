@@ -25,7 +25,11 @@ struct TemplateCands {
 };
 
 struct BackendStats {
-  double gpu_ms = 0;         // device time of template batches
+  // Sum over batches of the time from the previous completion on the same
+  // stream to this batch's completion event, counted only while batches are
+  // queued back to back (an idle stream restarts the chain): the busy span of
+  // the stream, not kernel time (rocprofv3 kernel traces give that).
+  double busy_span_ms = 0;
   double whiten_ms = 0;      // device time of the whitening step
   uint64_t templates = 0;
   uint64_t batches = 0;
@@ -33,6 +37,7 @@ struct BackendStats {
   uint64_t select_batches = 0;    // batches that ran with the bounded output
   uint64_t select_exits = 0;      // returns to the compacting path (floors rose)
   uint64_t list_dma_copies = 0;   // long candidate lists DMA-copied instead of read in place
+  uint64_t candidates = 0;        // above-threshold (bin, level, template) entries returned by the device
   uint64_t shared_series_batches = 0;  // batches that read another pipeline's series in place
   uint64_t peer_series_copies = 0;     // series taken device to device (peer / D2D), not from the host
 };

@@ -349,7 +349,6 @@ struct HipEngine::Impl {
   // (N/2 for even N, N for odd N); bluestein_kernels.hpp
   bool bs = false;
   uint32_t bs_Mb = 0;
-  uint32_t bs_nparts = 0;       // chirp-in workgroups per template (partial sums)
   DevBuf<float2> bs_a;          // [batch][L] chirp-in / convolution spectrum / A
   DevBuf<float2> bs_h;          // [L] FFT_L of the wrapped conjugate chirp
   DevBuf<float2> bs_chirp_hi, bs_chirp_lo;  // W_{2 Mb}
@@ -395,6 +394,12 @@ struct HipEngine::Impl {
   DevBuf<uint8_t> w_rmed;       // wide-window running-median scratch (whitening)
   DevBuf<float> ps;             // [batch][ps_stride]
   DevBuf<float> pyr;            // [batch][hs_pyr_stride(ps_stride)]: 8-bin maxima of the spectrum (pruned HS)
+  DevBuf<float> pyr1;           // the odd bins of cells pass 3 splits (p3_cells; zero elsewhere)
+  // pass 3 writes the 8-bin cell maxima of the spectrum it stores, so the
+  // harmonic sum does not re-read the spectrum for them (hs_cells_kernel).
+  // BRP_P3_CELLS=0/1; only with the three-pass FFT and direct 8-bin bounds
+  bool p3_cells = false;
+  bool cells_fused() const { return p3_cells && !bs && hs_prune && hs_cell_shift == 3 && hs_direct; }
   bool hs_prune = true;         // pruned harmonic sum (BRP_HS_FULL=1: every block exactly)
   int hs_cell_shift = 3;        // its bound cells: 8 bins (BRP_HS_CELL=4: 4 bins, tighter bounds but
                                 // 44 KB LDS / 125 VGPRs per workgroup: 16.4-16.7k vs 15.6-15.8k templates/s)
@@ -513,29 +518,33 @@ struct HipEngine::Impl {
   }
 
   // ---- chirp-z path
-  // y (bs_a) -> FFT_L -> * H, conj (bs_a) -> FFT_L -> conj * w / L = A (bs_a);
-  // pass 2 of the first transform reduces the template partial sums (delta)
-  hipError_t bs_convolve(int nb, bool templates) {
-    hipError_t e = bs_round(nb, 0, templates);
-    return e == hipSuccess ? bs_round(nb, 1, templates) : e;
+  // y (bs_a) -> FFT_L -> * H, conj (bs_a) -> FFT_L -> conj * w / L = A (bs_a)
+  // (whitening; the template path starts from the series: bs_template_in)
+  hipError_t bs_convolve(int nb) {
+    hipError_t e = bs_round(nb, 0);
+    return e == hipSuccess ? bs_round(nb, 1) : e;
   }
-  hipError_t bs_round(int nb, int round, bool templates) {
-    return bs_fft(nb, round == 0 ? hipk::C3_MULCONJ : hipk::C3_CHIRP, bs_a.p, templates && round == 0);
+  hipError_t bs_round(int nb, int round) {
+    return bs_fft(nb, round == 0 ? hipk::C3_MULCONJ : hipk::C3_CHIRP, bs_a.p);
   }
-  // one length-L transform of bs_a (passes 1, 2 and the epilogue of `mode`
-  // into out); reduce_delta: pass 2 also turns the chirp-in kernel's partial
-  // sums into the per-template padding mean
-  hipError_t bs_fft(int nb, hipk::Pass3CplxMode mode, float2* out, bool reduce_delta) {
-    const hipk::TwiddleTable tw = twt();
+  // one length-L transform of bs_a (passes 1, 2 and the epilogue of `mode` into out)
+  hipError_t bs_fft(int nb, hipk::Pass3CplxMode mode, float2* out) {
     hipk::Pass1Args a1{};
     a1.out = buf.p;
     a1.L2L3 = plan.L2 * plan.L3;
     a1.L3 = plan.L3;
-    a1.tw = tw;
+    a1.tw = twt();
     a1.tb = tables();
     a1.cplx_in = bs_a.p;
     hipError_t e = hipk::launch_pass1(plan, hipk::P1_COMPLEX, a1, nb, stream);
-    if (e != hipSuccess) return e;
+    return e == hipSuccess ? bs_fft_rest(nb, mode, out, 0) : e;
+  }
+  // passes 2 and 3 of a length-L transform in buf; n_partials > 0: pass 2
+  // also reduces pass 1's template partial sums (delta)
+  hipError_t bs_fft_rest(int nb, hipk::Pass3CplxMode mode, float2* out, uint32_t n_partials) {
+    const hipk::TwiddleTable tw = twt();
+    const bool reduce_delta = n_partials > 0;
+    hipError_t e;
     hipk::Pass2Args a2{};
     a2.buf = buf.p;
     a2.L1 = plan.L1;
@@ -545,7 +554,7 @@ struct HipEngine::Impl {
     a2.tb = tables();
     if (reduce_delta) {
       a2.partials = partials.p;
-      a2.n_partials = bs_nparts;
+      a2.n_partials = n_partials;
       a2.tmpl = tmpl.p;
       a2.delta = delta.p;
     }
@@ -570,7 +579,7 @@ struct HipEngine::Impl {
   hipError_t bs_make_h() {
     hipk::BsInArgs a = bs_in();
     hipError_t e = hipk::launch_bs_chirp_in(hipk::BS_IN_HCHIRP, a, 1, nullptr, stream);
-    return e == hipSuccess ? bs_fft(1, hipk::C3_PLAIN, bs_h.p, false) : e;
+    return e == hipSuccess ? bs_fft(1, hipk::C3_PLAIN, bs_h.p) : e;
   }
   hipk::BsInArgs bs_in() const {
     hipk::BsInArgs a{};
@@ -581,18 +590,27 @@ struct HipEngine::Impl {
     a.chirp = chirpt();
     return a;
   }
-  // template spectra of a batch: resampling + chirp, the two convolution
-  // rounds, power spectrum (bins k < limit into ps_out [nb][stride])
+  // template spectra of a batch: pass 1 of the first convolution transform
+  // straight from the series (resampling, centring, chirp: P1_CHIRP*), its
+  // passes 2 and 3 (* H), the second transform, the power spectrum (bins
+  // k < limit into ps_out [nb][stride])
   hipError_t bs_template_in(int nb, uint32_t* reset) {
-    hipk::BsInArgs a = bs_in();
-    a.series = series_in();
-    a.n_unpadded = g.n_unpadded;
-    a.tmpl = tmpl.p;
-    a.partials = partials.p;
-    a.reset = reset;
-    return hipk::launch_bs_chirp_in(bs_Mb == g.nsamples ? hipk::BS_IN_RESAMPLE1 : hipk::BS_IN_RESAMPLE2, a, nb, nullptr,
-                                    stream);
+    hipk::Pass1Args a1{};
+    a1.out = buf.p;
+    a1.L2L3 = plan.L2 * plan.L3;
+    a1.L3 = plan.L3;
+    a1.tw = twt();
+    a1.tb = tables();
+    a1.series = series_in();
+    a1.n_unpadded = g.n_unpadded;
+    a1.tmpl = tmpl.p;
+    a1.partials = partials.p;
+    a1.reset = reset;
+    a1.chirp = chirpt();
+    a1.Mb = bs_Mb;
+    return hipk::launch_pass1(plan, bs_Mb == g.nsamples ? hipk::P1_CHIRP1 : hipk::P1_CHIRP2, a1, nb, stream);
   }
+  hipError_t bs_template_round0(int nb) { return bs_fft_rest(nb, hipk::C3_MULCONJ, bs_a.p, plan.wg1()); }
   hipError_t bs_template_power(int nb, float* ps_out, _Float16* ps16_out, uint32_t stride, uint32_t limit) {
     hipk::BsPowerArgs ap{};
     ap.A = bs_a.p;
@@ -611,7 +629,8 @@ struct HipEngine::Impl {
   }
   hipError_t bs_template_spectra(int nb, float* ps_out, _Float16* ps16_out, uint32_t stride, uint32_t limit) {
     hipError_t e = bs_template_in(nb, nullptr);
-    if (e == hipSuccess) e = bs_convolve(nb, true);
+    if (e == hipSuccess) e = bs_template_round0(nb);
+    if (e == hipSuccess) e = bs_round(nb, 1);
     return e == hipSuccess ? bs_template_power(nb, ps_out, ps16_out, stride, limit) : e;
   }
 
@@ -653,7 +672,7 @@ struct HipEngine::Impl {
         return hipk::launch_pass1(plan, hipk::P1_RESAMPLE, a1, nb, stream);
       }
       case kPass2: {
-        if (bs) return bs_round(nb, 0, true);
+        if (bs) return bs_template_round0(nb);
         hipk::Pass2Args a2{};
         a2.buf = buf.p;
         a2.L1 = plan.L1;
@@ -669,7 +688,7 @@ struct HipEngine::Impl {
       }
       case kPass3: {
         if (bs) {
-          const hipError_t e3 = bs_round(nb, 1, true);
+          const hipError_t e3 = bs_round(nb, 1);
           if (e3 != hipSuccess) return e3;
           return bs_template_power(nb, ps.p, ps_fp16 ? reinterpret_cast<_Float16*>(ps.p) : nullptr, ps_stride,
                                    std::min(g.harmonic_idx_hi, g.fft_size));
@@ -690,6 +709,11 @@ struct HipEngine::Impl {
         a3.norm = static_cast<float>(1.0 / g.nsamples);
         a3.tmpl = tmpl.p;
         a3.delta = delta.p;
+        if (cells_fused() && !select_mode) {
+          a3.cells = pyr.p;
+          a3.cells1 = pyr1.p;
+          a3.cells_stride = hipk::hs_pyr_stride(ps_stride);
+        }
         return hipk::launch_pass3(plan, hipk::P3_POWER, a3, nb, stream);
       }
       case kHarmonic: {
@@ -713,6 +737,8 @@ struct HipEngine::Impl {
         ah.pyr_stride = hipk::hs_pyr_stride(ps_stride);
         ah.key_base = key_base;
         ah.bin_bits = bin_bits;
+        ah.cells_ready = cells_fused();
+        ah.pyr1 = pyr1.p;
         if (select_mode) {
           hipk::HsSelectArgs sa{};
           sa.dense = sel_dense.p;
@@ -1023,8 +1049,20 @@ int HipEngine::setup_impl(const SearchGeometry& g, const float* host_series, con
   d.hs_direct = std::getenv("BRP_HS_DIRECT") == nullptr || std::atoi(std::getenv("BRP_HS_DIRECT")) != 0;
   d.hs_xcd = std::getenv("BRP_HS_XCD") != nullptr && std::atoi(std::getenv("BRP_HS_XCD")) == 1;
   if ((rc = d.pyr.alloc(B * hipk::hs_pyr_stride(d.ps_stride)))) return rc;
-  d.bs_nparts = d.bs ? hipk::bs_chirp_in_blocks(d.plan.M) : 0;
-  if ((rc = d.partials.alloc(B * std::max(d.plan.wg1(), d.bs_nparts)))) return rc;
+  {
+    const char* e = std::getenv("BRP_P3_CELLS");
+    d.p3_cells = e != nullptr && std::atoi(e) != 0;
+  }
+  if (d.cells_fused()) {
+    // cells pass 3 never writes (past the limit; the odd-bin array outside
+    // split cells) must read as 0: cleared once, rewritten identically per template
+    if ((rc = d.pyr1.alloc(B * hipk::hs_pyr_stride(d.ps_stride)))) return rc;
+    BRP_HIP_CHECK(hipMemsetAsync(d.pyr.p, 0, d.pyr.n * sizeof(float), d.stream), RADPUL_HIP_MEM_COPY_HOST_DEVICE);
+    BRP_HIP_CHECK(hipMemsetAsync(d.pyr1.p, 0, d.pyr1.n * sizeof(float), d.stream), RADPUL_HIP_MEM_COPY_HOST_DEVICE);
+  } else {
+    d.pyr1.release();
+  }
+  if ((rc = d.partials.alloc(B * d.plan.wg1()))) return rc;  // pass-1 partial sums (P1_RESAMPLE / P1_CHIRP*)
   if (d.bs) {
     if ((rc = d.bs_a.alloc(B * d.plan.M)) || (rc = d.bs_h.alloc(d.plan.M))) return rc;
     const auto& ch = twiddles_cached(2ull * d.bs_Mb);
@@ -1106,7 +1144,8 @@ int HipEngine::upload_series(const std::vector<float>& series, float mu0) { retu
 int HipEngine::adopt_series(const HipEngine& src) {
   Impl& d = *impl_;
   const Impl& s = *src.impl_;
-  if (!d.ready || !s.ready || d.device != s.device || d.slots != 1 || s.slots != 1 || !same_geometry(d.g, s.g))
+  // any number of work-unit slots (multi-WU batching), the same on both sides
+  if (!d.ready || !s.ready || d.device != s.device || d.slots != s.slots || !same_geometry(d.g, s.g))
     return RADPUL_EVAL;
   trace::Range range("brp:adopt_series");
   BRP_HIP_CHECK(hipSetDevice(d.device), RADPUL_HIP_DEVICE_SET);
@@ -1128,7 +1167,8 @@ int HipEngine::adopt_series(const HipEngine& src) {
     d.adopted_token.reset();
   }
   if (!share)
-    BRP_HIP_CHECK(copy_sync(d.series.p, s.series.p, d.g.n_unpadded * sizeof(float), hipMemcpyDeviceToDevice, d.stream),
+    BRP_HIP_CHECK(copy_sync(d.series.p, s.series_in(), static_cast<size_t>(d.slots) * d.g.n_unpadded * sizeof(float),
+                            hipMemcpyDeviceToDevice, d.stream),
                   RADPUL_HIP_MEM_COPY_HOST_DEVICE);
   return 0;
 }
@@ -1172,6 +1212,8 @@ bool HipEngine::prepared_for(const SearchGeometry& g) const {
   return impl_->ready && impl_->slots == 1 && same_geometry(impl_->g, g);
 }
 
+bool HipEngine::ready_for(const SearchGeometry& g) const { return impl_->ready && same_geometry(impl_->g, g); }
+
 int HipEngine::whiten(const SearchOptions& opt, const std::vector<ZapRange>& zaps, std::vector<float>& series,
                       uint32_t slot, bool copy_back) {
   Impl& d = *impl_;
@@ -1206,7 +1248,7 @@ int HipEngine::whiten(const SearchOptions& opt, const std::vector<ZapRange>& zap
     ab.n_real = g.n_unpadded;
     BRP_HIP_CHECK(hipk::launch_bs_chirp_in(odd ? hipk::BS_IN_REAL1 : hipk::BS_IN_REAL2, ab, 1, nullptr, s),
                   RADPUL_HIP_KERNEL_INVOKE);
-    BRP_HIP_CHECK(d.bs_convolve(1, false), RADPUL_HIP_KERNEL_INVOKE);
+    BRP_HIP_CHECK(d.bs_convolve(1), RADPUL_HIP_KERNEL_INVOKE);
     BRP_HIP_CHECK(hipk::launch_bs_spec(d.bs_a.p, d.bs_Mb, g.nsamples, tw, fft_size, spec.p, s),
                   RADPUL_HIP_KERNEL_INVOKE);
   } else {
@@ -1302,7 +1344,7 @@ int HipEngine::whiten(const SearchOptions& opt, const std::vector<ZapRange>& zap
     ab.fft_size = fft_size;
     BRP_HIP_CHECK(hipk::launch_bs_chirp_in(odd ? hipk::BS_IN_HERM_CONJ : hipk::BS_IN_CONJ, ab, 1, nullptr, s),
                   RADPUL_HIP_KERNEL_INVOKE);
-    BRP_HIP_CHECK(d.bs_convolve(1, false), RADPUL_HIP_KERNEL_INVOKE);
+    BRP_HIP_CHECK(d.bs_convolve(1), RADPUL_HIP_KERNEL_INVOKE);
     BRP_HIP_CHECK(hipk::launch_bs_real_out(d.bs_a.p, d.bs_Mb, g.nsamples, inv_scale, slot_series, g.n_unpadded, s),
                   RADPUL_HIP_KERNEL_INVOKE);
   } else {
@@ -1458,7 +1500,7 @@ int HipEngine::complete(std::vector<TemplateCands>& out) {
   float ms = 0;
   if (d.prev_done != nullptr && max_in_flight() < Impl::kIoSlots) (void)hipEventElapsedTime(&ms, d.prev_done, o.ev1);
   d.prev_done = d.io_busy() ? o.ev1 : nullptr;  // an idle stream restarts the chain
-  d.st.gpu_ms += ms;
+  d.st.busy_span_ms += ms;
   d.st.batches += 1;
   if (d.shared_series != nullptr) d.st.shared_series_batches += 1;
   d.st.templates += nb;
@@ -1498,6 +1540,7 @@ int HipEngine::complete(std::vector<TemplateCands>& out) {
     d.st.select_exits += 1;
   }
   if (ran_select) d.st.select_batches += 1;
+  d.st.candidates += cnt;
   const uint2* src = o.h_cands_p + 1;
   std::vector<uint2> extra;
   // beyond kcopy entries a DMA copy of the list beats reading it in place

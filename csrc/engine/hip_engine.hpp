@@ -23,8 +23,8 @@ class HipEngine {
   int setup(const SearchGeometry& g, const std::vector<float>& series, float mu0);
   int upload_series(const std::vector<float>& series, float mu0);
   // Re-setup for the next pass over the same geometry from `src`'s (whitened)
-  // series: `src` and this engine share a device and this engine was set up
-  // before. The pipeline reads `src`'s series in place (one copy in the
+  // series: `src` and this engine share a device, have the same number of WU
+  // slots, and this engine was set up before. The pipeline reads `src`'s series in place (one copy in the
   // Infinity Cache for all pipelines; `src` must outlive the search pass), or
   // copies it device to device with BRP_SHARE_SERIES=0. setup(), load_slot()
   // and whiten() return to the engine's own buffer. RADPUL_EVAL when not applicable.
@@ -49,6 +49,8 @@ class HipEngine {
              uint32_t slot = 0, bool copy_back = true);
   // set up (buffers, plan, graphs) for this geometry with one WU slot
   bool prepared_for(const SearchGeometry& g) const;
+  // set up for this geometry with any number of slots (multi-WU batching)
+  bool ready_for(const SearchGeometry& g) const;
   int process(const TemplateInput* t, int n, const float thr[kNumHarmonicLevels], std::vector<TemplateCands>& out);
   // per-template thresholds thr[i * thr_stride + h] (thr_stride 0: shared)
   int process(const TemplateInput* t, int n, const float* thr, int thr_stride, std::vector<TemplateCands>& out);

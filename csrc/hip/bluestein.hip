@@ -19,33 +19,7 @@ __device__ __forceinline__ float2 chirp_w(const TwiddleTable& t, uint32_t n) {
 
 template <int MODE>
 __global__ void __launch_bounds__(kThreads) bs_chirp_in_kernel(BsInArgs a) {
-  __shared__ float lut_s[kLutSize], lut_c[kLutSize];
-  __shared__ double red[kThreads / kWave + 1];
-  constexpr bool kTemplate = MODE == BS_IN_RESAMPLE2 || MODE == BS_IN_RESAMPLE1;
   const int b = blockIdx.y;
-  if (a.reset != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *a.reset = 0;
-  TemplateDev td{};
-  const float* series = nullptr;
-  if constexpr (kTemplate) {
-    for (int i = threadIdx.x; i < kLutSize; i += kThreads) {
-      lut_s[i] = kSinLut[i];
-      lut_c[i] = kCosLut[i];
-    }
-    __syncthreads();
-    td = a.tmpl[b];
-    series = a.series + static_cast<size_t>(td.wu) * a.n_unpadded;
-  }
-  const bool fast = a.n_unpadded <= (1u << 23);
-  const int last = static_cast<int>(a.n_unpadded) - 1;
-  // centred resampled sample m (zero beyond n_steps: the mean padding is
-  // added analytically in bs_power_kernel)
-  auto sample = [&](uint32_t m) -> float {
-    if (m >= td.n_steps) return 0.0f;
-    const float dt = resamp_del_t(m, td.p, lut_s, lut_c);
-    const int i = min(max(fast ? resamp_nearest_f(m, dt) : resamp_nearest(m, dt), 0), last);
-    return series[i] - td.mu0;
-  };
-  float fsum = 0.0f;
   float2* y = a.y + static_cast<size_t>(b) * a.L;
   const uint32_t n0 = (blockIdx.x * kPerThread) * kThreads + threadIdx.x;
 #pragma unroll
@@ -59,13 +33,7 @@ __global__ void __launch_bounds__(kThreads) bs_chirp_in_kernel(BsInArgs a) {
       else if (a.L - n < a.Mb) v = conjf2(chirp_w(a.chirp, a.L - n));
     } else if (n < a.Mb) {
       float2 x;
-      if (MODE == BS_IN_RESAMPLE2) {
-        x = make_float2(sample(2 * n), sample(2 * n + 1));
-        fsum += x.x + x.y;
-      } else if (MODE == BS_IN_RESAMPLE1) {
-        x = make_float2(sample(n), 0.0f);
-        fsum += x.x;
-      } else if (MODE == BS_IN_REAL2) {
+      if (MODE == BS_IN_REAL2) {
         x = make_float2(2 * n < a.n_real ? a.real_in[2 * n] : 0.0f, 2 * n + 1 < a.n_real ? a.real_in[2 * n + 1] : 0.0f);
       } else if (MODE == BS_IN_REAL1) {
         x = make_float2(n < a.n_real ? a.real_in[n] : 0.0f, 0.0f);
@@ -85,10 +53,6 @@ __global__ void __launch_bounds__(kThreads) bs_chirp_in_kernel(BsInArgs a) {
       v = cmul(x, chirp_w(a.chirp, n));
     }
     y[n] = v;
-  }
-  if constexpr (kTemplate) {
-    const double tot = block_sum<kThreads>(static_cast<double>(fsum), red);
-    if (threadIdx.x == 0) a.partials[static_cast<size_t>(b) * gridDim.x + blockIdx.x] = tot;
   }
 }
 
@@ -162,8 +126,6 @@ hipError_t launch_bs_chirp_in(BsInMode mode, const BsInArgs& a, int batch, uint3
   switch (mode) {
 #define BRP_BS_CASE(M) \
   case M: hipLaunchKernelGGL((bs_chirp_in_kernel<M>), grid, dim3(kThreads), 0, s, a); break;
-    BRP_BS_CASE(BS_IN_RESAMPLE2)
-    BRP_BS_CASE(BS_IN_RESAMPLE1)
     BRP_BS_CASE(BS_IN_REAL2)
     BRP_BS_CASE(BS_IN_REAL1)
     BRP_BS_CASE(BS_IN_CONJ)

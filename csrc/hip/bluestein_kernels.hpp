@@ -9,7 +9,7 @@
 //   A_k = w_k * sum_n (a_n w_n) conj(w_{k-n}),   w_n = exp(-pi i n^2 / Mb),
 // a circular convolution of length L >= 2 Mb - 1 computed with two length-L
 // transforms of the smooth three-pass FFT:
-//   y = chirp(a) (zero padded)          bs_chirp_in_kernel
+//   y = chirp(a) (zero padded)          bs_chirp_in_kernel (templates: pass 1, P1_CHIRP*)
 //   FFT_L(y) * H -> conj                 pass 1, 2, pass3_cplx (C3_MULCONJ)
 //   FFT_L again -> conj * w / L          pass 1, 2, pass3_cplx (C3_CHIRP)
 // with H = FFT_L(conj chirp, wrapped) precomputed once per plan. The consumers
@@ -27,9 +27,9 @@
 namespace brp {
 namespace hipk {
 
+// (templates never materialise their chirp-multiplied input: pass 1 computes
+// it from the series, Pass1Mode P1_CHIRP2 / P1_CHIRP1)
 enum BsInMode : int {
-  BS_IN_RESAMPLE2 = 0,  // template, even N: (x[2n], x[2n+1]) resampled and centred
-  BS_IN_RESAMPLE1 = 1,  // template, odd N: x[n]
   BS_IN_REAL2 = 2,      // whitening forward, even N: zero-padded real series pairs
   BS_IN_REAL1 = 3,      // whitening forward, odd N
   BS_IN_CONJ = 4,       // whitening inverse, even N: conj(z[n]) of the tangled half spectrum
@@ -42,12 +42,6 @@ struct BsInArgs {
   uint32_t L, Mb;              // convolution length, DFT length
   uint32_t nsamples;           // N
   TwiddleTable chirp;          // W_{2 Mb}
-  // templates
-  const float* series;         // [slots][n_unpadded]
-  uint32_t n_unpadded;
-  const TemplateDev* tmpl;     // [batch]
-  double* partials;            // [batch][gridDim.x] sums of the centred samples
-  uint32_t* reset;             // candidate counter zeroed by workgroup (0, 0) (may be null)
   // whitening
   const float* real_in;        // BS_IN_REAL*: n_real samples, zero beyond
   uint32_t n_real;

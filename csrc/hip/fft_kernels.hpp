@@ -41,6 +41,11 @@ enum Pass1Mode : int {
   P1_REAL = 1,       // zero-padded real series
   P1_COMPLEX_CONJ = 2,  // complex input, conjugated (inverse transform)
   P1_COMPLEX = 3,       // complex input as is (chirp-z convolutions, bluestein_kernels.hpp)
+  // chirp-z template transforms (bluestein_kernels.hpp): the resampled,
+  // centred series times the chirp w_n for n < Mb, zero beyond, straight from
+  // the series (the chirp-multiplied input is never materialised)
+  P1_CHIRP2 = 4,        // even N: (x[2n], x[2n+1]) w_n
+  P1_CHIRP1 = 5,        // odd N: x[n] w_n
 };
 
 struct Pass1Args {
@@ -59,6 +64,9 @@ struct Pass1Args {
   uint32_t n_real;
   // P1_COMPLEX_CONJ, P1_COMPLEX: [batch][M]
   const float2* cplx_in;
+  // P1_CHIRP*: chirp W_{2 Mb}^{n^2} of the length-Mb DFT (also uses series/tmpl/partials)
+  TwiddleTable chirp;
+  uint32_t Mb;
 };
 
 struct Pass2Args {
@@ -97,6 +105,14 @@ struct Pass3Args {
   const double* delta;         // [batch] mean-padding correction (pass 2)
   // P3_COMPLEX
   float2* spec;                // fft_size complex bins
+  // P3_POWER*, optional: 8-bin maxima of the written spectrum for the pruned
+  // harmonic sum (replaces hs_cells_kernel's re-read of the spectrum). A cell
+  // whose 8 bins come from two row groups (the mirror rows of the untangle
+  // are one bin off the 8-bin grid) is split: 7 bins into `cells`, the odd bin
+  // into `cells1` (0 everywhere else); the harmonic sum reads max of both.
+  float* cells;                // [batch][cells_stride] or nullptr
+  float* cells1;               // [batch][cells_stride]
+  uint32_t cells_stride;
 };
 
 // plain row pass of the inverse transform: conj, scale, write the first

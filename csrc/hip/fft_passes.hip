@@ -112,6 +112,41 @@ __global__ void __launch_bounds__(kNcol * tpc_for<L>()) pass1_kernel(Pass1Args a
     const float fsum = pruned ? gather(std::integral_constant<int, kPerPruned>{})
                               : gather(std::integral_constant<int, kPer>{});
     sum = static_cast<double>(fsum);
+  } else if (MODE == P1_CHIRP2 || MODE == P1_CHIRP1) {
+    __shared__ float lut_s[kLutSize], lut_c[kLutSize];
+    for (int i = threadIdx.x; i < kLutSize; i += NT) {
+      lut_s[i] = kSinLut[i];
+      lut_c[i] = kCosLut[i];
+    }
+    __syncthreads();
+    const bool fast = a.n_unpadded <= (1u << 23);
+    const TemplateDev td = a.tmpl[b];
+    const float* series = a.series + static_cast<size_t>(td.wu) * a.n_unpadded;
+    const int last = static_cast<int>(a.n_unpadded) - 1;
+    // the convolution input is zero from Mb on (L >= 2 Mb - 1): with
+    // Mb <= (L / R0) L2L3 the rows n1 >= L / R0 are all zero (run_pruned)
+    constexpr int kR0 = BlockFFT<L, kNcol, TPC, false>::kFirstRadix;
+    pruned = static_cast<uint64_t>(L / kR0) * a.L2L3 >= a.Mb;
+    const int rows_valid = pruned ? L / kR0 : L;
+    auto sample = [&](uint32_t m) -> float {
+      if (m >= td.n_steps) return 0.0f;
+      const float dt = resamp_del_t(m, td.p, lut_s, lut_c);
+      const int i = min(max(fast ? resamp_nearest_f(m, dt) : resamp_nearest(m, dt), 0), last);
+      return series[i] - td.mu0;
+    };
+    float fsum = 0.0f;
+    for (int r = tj; r < rows_valid; r += TPC) {
+      const uint32_t n = r * a.L2L3 + col_base + c;
+      float2 v = make_float2(0.0f, 0.0f);
+      if (n < a.Mb) {
+        const float2 x = MODE == P1_CHIRP2 ? make_float2(sample(2 * n), sample(2 * n + 1))
+                                           : make_float2(sample(n), 0.0f);
+        fsum += x.x + x.y;
+        v = cmul(x, tw_lookup(a.chirp, static_cast<uint64_t>(n) * n));  // W_{2Mb}^{n^2 mod 2Mb}
+      }
+      data[Lay::idx(r, c)] = v;
+    }
+    sum = static_cast<double>(fsum);
   } else if (MODE == P1_REAL) {
     for (int r = tj; r < L; r += TPC) {
       const uint32_t n = r * a.L2L3 + col_base + c;
@@ -137,7 +172,7 @@ __global__ void __launch_bounds__(kNcol * tpc_for<L>()) pass1_kernel(Pass1Args a
     const float2 v = cmul(data[Lay::idx(k1, c)], two[k1]);
     out[static_cast<size_t>(k1) * a.L2L3 + col_base + c] = v;
   }
-  if (MODE == P1_RESAMPLE) {
+  if (MODE == P1_RESAMPLE || MODE == P1_CHIRP2 || MODE == P1_CHIRP1) {
     const double tot = block_sum<NT>(sum, red);
     if (threadIdx.x == 0) a.partials[static_cast<size_t>(b) * gridDim.x + blockIdx.x] = tot;
   }
@@ -543,21 +578,30 @@ struct P3Emit {
     }
     return (x.x * x.x + x.y * x.y) * a.norm;
   }
-  __device__ __forceinline__ void store(uint32_t k, float p) const {
+  // stores bin k's power; returns the value the spectrum holds (fp16-rounded in P3_POWER16)
+  __device__ __forceinline__ float store(uint32_t k, float p) const {
     const size_t o = static_cast<size_t>(b) * a.ps_stride + k;
     // fp16 spectrum (config 5) saturates at the largest finite half: a strong
     // line stays a (clamped) candidate instead of an inf in the sums
-    if (MODE == P3_POWER16) a.ps16[o] = static_cast<_Float16>(fminf(p, 65504.0f));
-    else a.ps[o] = p;
+    if (MODE == P3_POWER16) {
+      const _Float16 h = static_cast<_Float16>(fminf(p, 65504.0f));
+      a.ps16[o] = h;
+      return static_cast<float>(h);
+    }
+    a.ps[o] = p;
+    return p;
   }
-  __device__ __forceinline__ void operator()(uint32_t k, float2 x, float2 tk, float2 ta) const {
-    if (k >= a.limit) return;
-    if (kPower) store(k, power(k, x, tk, ta));
-    else a.spec[k] = x;
+  // the spectrum value written for bin k (0 for bins past the limit: the
+  // harmonic sum never reads them, and the cell maxima count them as 0)
+  __device__ __forceinline__ float operator()(uint32_t k, float2 x, float2 tk, float2 ta) const {
+    if (k >= a.limit) return 0.0f;
+    if (kPower) return store(k, power(k, x, tk, ta));
+    a.spec[k] = x;
+    return 0.0f;
   }
   // Nyquist bin M: X_M = Re Z_0 - Im Z_0
-  __device__ __forceinline__ void nyquist(float2 z0, uint32_t n_s) const {
-    if (a.M >= a.limit) return;
+  __device__ __forceinline__ float nyquist(float2 z0, uint32_t n_s) const {
+    if (a.M >= a.limit) return 0.0f;
     float2 x = make_float2(z0.x - z0.y, 0.0f);
     if (kPower) {
       if (correct) {
@@ -565,12 +609,10 @@ struct P3Emit {
         x = make_float2(x.x + dS * sp.x, x.y + dS * sp.y);
       }
       const float pm = (x.x * x.x + x.y * x.y) * a.norm;
-      const size_t o = static_cast<size_t>(b) * a.ps_stride + a.M;
-      if (MODE == P3_POWER16) a.ps16[o] = static_cast<_Float16>(fminf(pm, 65504.0f));
-      else a.ps[o] = pm;
-    } else {
-      a.spec[a.M] = x;
+      return store(a.M, pm);
     }
+    a.spec[a.M] = x;
+    return 0.0f;
   }
 };
 
@@ -702,6 +744,75 @@ __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Arg
   // rotations: W_2N^k and W_2N^{n_s k} are stepped by one complex multiply per
   // bin (a few ulp over L / kStreams steps) instead of two table products.
   static_assert(L % kStreams == 0, "whole untangle iterations");
+  // Fused 8-bin cell maxima (Pass3Args::cells): the ROWS = 8 lanes s of one
+  // k3 stream hold bins c0 .. c0 + 7 (+ C k3): one whole cell (c0, C are
+  // multiples of 8). Their mirror bins C - c0 - s (+ C (L - 1 - k3)) are one
+  // off the grid: lanes 1..7 fill 7 bins of cell (C - c0) / 8 - 1 (`cells`),
+  // lane 0 the first bin of the next cell (`cells1`). Every cell has exactly
+  // one writer per array, so no atomics; cells past the limit are skipped.
+  static_assert(!kPower || ROWS == 8, "fused cells: one 8-bin cell per 8-lane group");
+  const bool cells = kPower && a.cells != nullptr;
+  float* const cl = cells ? a.cells + static_cast<size_t>(b) * a.cells_stride : nullptr;
+  float* const cl1 = cells ? a.cells1 + static_cast<size_t>(b) * a.cells_stride : nullptr;
+  const uint32_t nlim = (a.limit + 7) / 8;  // cells holding at least one written bin
+  auto group8_max = [](float v) {
+    v = fmaxf(v, __shfl_xor(v, 1, kWave));
+    v = fmaxf(v, __shfl_xor(v, 2, kWave));
+    return fmaxf(v, __shfl_xor(v, 4, kWave));
+  };
+  const uint32_t c0u = c0;
+  if (cells) {
+    // wave-uniform structure: every lane runs the same iterations (rows above
+    // C/2 contribute 0), so the 8-lane shuffles see all their partners
+    // twiddles stepped exactly as in the plain loop below (same powers, bit for bit)
+    float2 tk = cmul(rt.t1, w4(static_cast<uint32_t>(t)));
+    const float2 tk_step = w4(static_cast<uint32_t>(kStreams));
+    float2 ta = make_float2(0.f, 0.f), ta_step = make_float2(1.f, 0.f);
+    if (correct) {
+      ta = cmul(rt.ta, w4((n_s * static_cast<uint32_t>(t)) % L4));
+      ta_step = w4((n_s * static_cast<uint32_t>(kStreams)) % L4);
+    }
+#pragma unroll
+    for (int it = 0; it < L / kStreams; ++it) {
+      const int k3 = t + it * kStreams;
+      if (it > 0) {
+        tk = cmul(tk, tk_step);
+        if (correct) ta = cmul(ta, ta_step);
+      }
+      float vd = 0.0f, vm = 0.0f;
+      if (c <= half) {
+        const float2 zk = data[Lay::idx(k3, s)];
+        const int k3m = (c == 0) ? (L - k3) % L : L - 1 - k3;
+        const float2 zm = data[Lay::idx(k3m, c == 0 ? s : ROWS + s)];
+        const uint32_t k = c + a.C * static_cast<uint32_t>(k3);
+        const float2 w = cmul(tk, tk);
+        vd = emit(k, untangle_w(zk, zm, w), tk, ta);
+        if (c != 0 && c != half) {
+          const float2 wm = make_float2(-w.x, w.y);
+          vm = emit(a.M - k, untangle_w(zm, zk, wm), make_float2(-tk.y, -tk.x), rot_mi(conjf2(ta), n_s));
+        }
+        if (c == 0 && k3 == 0) {
+          const float vn = emit.nyquist(zk, n_s);
+          if (a.M / 8 < nlim) cl1[a.M / 8] = vn;  // bin M alone in its cell
+        }
+      }
+      const float md = group8_max(vd);
+      const float m7 = group8_max(s == 0 ? 0.0f : vm);
+      if (s == 0 && c0u <= half) {
+        const uint32_t xd = (c0u + a.C * static_cast<uint32_t>(k3)) >> 3;
+        if (xd < nlim) {
+          if (c0u < half) cl[xd] = md;
+          else cl1[xd] = md;  // row C/2 alone: the odd bin of its cell
+        }
+        if (c0u < half) {
+          const uint32_t xm = (a.C - c0u + a.C * static_cast<uint32_t>(L - 1 - k3)) >> 3;  // cell of bin C - c0
+          if (xm - 1 < nlim) cl[xm - 1] = m7;
+          if (c0u != 0 && xm < nlim) cl1[xm] = vm;
+        }
+      }
+    }
+    return;
+  }
   if (c <= half) {
     float2 tk = cmul(rt.t1, w4(static_cast<uint32_t>(t)));  // W_2N^k for k3 = t
     const float2 tk_step = w4(static_cast<uint32_t>(kStreams));
@@ -858,6 +969,8 @@ hipError_t launch_pass1(const FFTPlan3& plan, Pass1Mode mode, const Pass1Args& a
     if (mode == P1_RESAMPLE) hipLaunchKernelGGL((pass1_kernel<n, P1_RESAMPLE>), grid, block, 0, s, a); \
     else if (mode == P1_REAL) hipLaunchKernelGGL((pass1_kernel<n, P1_REAL>), grid, block, 0, s, a);    \
     else if (mode == P1_COMPLEX) hipLaunchKernelGGL((pass1_kernel<n, P1_COMPLEX>), grid, block, 0, s, a); \
+    else if (mode == P1_CHIRP2) hipLaunchKernelGGL((pass1_kernel<n, P1_CHIRP2>), grid, block, 0, s, a);   \
+    else if (mode == P1_CHIRP1) hipLaunchKernelGGL((pass1_kernel<n, P1_CHIRP1>), grid, block, 0, s, a);   \
     else hipLaunchKernelGGL((pass1_kernel<n, P1_COMPLEX_CONJ>), grid, block, 0, s, a);                 \
     break;                                                                                            \
   }

@@ -102,3 +102,47 @@ def test_app_any_padding_runs_on_gpu(brp, gpu, tmp_path):
     assert "chirp-z transform" in r.stderr and "CPU backend" not in r.stderr
     lines, done = brp.read_results(str(tmp_path / "r.cand"))
     assert done and lines
+
+
+@pytest.mark.parametrize("padding", [2.7, 2.9])
+def test_power_spectrum_bench_size(brp, gpu, padding):
+    """Production size: the shipped 2^22-sample WU at -P 2.7 (N = 11 324 621,
+    odd: a chirp-z DFT of length N over L >= 2N - 1) and -P 2.9 (N = 12 163 482,
+    N/2 = 3 * 2 027 247: the packed even path). The device spectrum of two
+    templates against the CPU double-precision spectrum, same bound as the
+    small lengths (the fp32 convolution error grows with L)."""
+    from conftest import WU
+
+    hdr, series, _ = brp.read_work_unit(str(WU))
+    geom = brp.derive_geometry(hdr, dict(f0=400.0, padding=padding, fA=0.08, window=1000))
+    N = geom["nsamples"]
+    assert brp.fft_plan(N // 2) is None or N % 2, N
+    eng = brp.HipEngine()
+    eng.init(0, 1)
+    eng.setup(geom, series, float(np.mean(series)))
+    for P, tau, psi in ((1046.6, 0.0547, 4.48), (2000.0, 0.3, 1.0)):
+        ps_g, ns_g = eng.power_spectrum(P, tau, psi)
+        xr, ns_c, _ = brp.cpu_resample(series, geom, P, tau, psi)
+        ps_c = brp.cpu_power_spectrum(xr, geom["fft_size"])
+        assert ns_g == ns_c
+        scale = float(np.mean(ps_c[1:]))
+        err = np.abs(ps_g.astype(np.float64) - ps_c)[1:] / np.maximum(ps_c[1:], scale)
+        assert err.max() < 2e-4, (N, padding, err.max(), int(np.argmax(err)) + 1)
+
+
+def test_bench_wu_p27_prefix_vs_cpu_golden(brp, gpu):
+    """The shipped WU at -P 2.7 -W (chirp-z path at bench size), first 50
+    templates, against the CPU golden model (tools/make_golden.py --end 50
+    --padding 2.7)."""
+    from conftest import BANK, ROOT, WU, ZAP
+    from test_gpu_search import _compare_tables
+
+    cfg = SearchConfig.benchmark(str(WU), str(BANK), str(ZAP), batch=1)
+    cfg.padding = 2.7
+    g = BRPSearch(cfg, pipelines=3).run(begin=0, end=50, write_output=False, use_checkpoint=False)
+    assert g.templates_run == 50 and g.geometry["nsamples"] == 11324621
+    gold = brp.CandidateTable()
+    gold.from_bytes(np.frombuffer((ROOT / "data" / "golden" / "bench_wu_cpu_table_first50_P2.7.bin").read_bytes(),
+                                  dtype=np.uint8).copy())
+    assert sum(1 for e in gold.entries() if e[5] > 0) > 20
+    _compare_tables(g.table, gold)
