@@ -54,6 +54,7 @@ struct MultiSession::Impl {
   uint32_t block_batches = 0;  // 0: BRP_MULTI_BLOCK / default
   bool shape_mismatch = false;
   SearchInfo info;
+  std::vector<std::shared_ptr<void>> pins;  // page-locked WU sample buffers (direct uploads)
 };
 
 uint32_t multi_block_templates(int B, uint32_t total) {
@@ -153,11 +154,20 @@ int MultiSession::prepare() {
   for (auto& e : d.engines) all_same_device = all_same_device && e->device() == d.engines[0]->device();
   HipEngine& e0 = *d.engines[0];
   for (size_t k = 0; k < d.wus.size(); ++k) {
-    std::vector<float>& s = prepared[k];
-    s = d.wus[k].samples;
+    // Whitening on one device only reads the raw samples (uploaded straight
+    // from the page-locked WU buffer) and resets the padding offset to 0, so
+    // neither a host copy nor the 4M-sample mean is needed then; otherwise the
+    // (whitened) host copy feeds the engines on other devices.
+    const bool direct = d.opt.white && all_same_device;
+    if (!direct) prepared[k] = d.wus[k].samples;
+    std::vector<float>& s = direct ? d.wus[k].samples : prepared[k];
+    if (direct && d.pins.size() < d.wus.size()) d.pins.resize(d.wus.size());
+    if (direct && !d.pins[k]) d.pins[k] = hip_pin_host(s.data(), s.size() * sizeof(float));
     double mean = 0.0;
-    for (float v : s) mean += v;
-    mean = s.empty() ? 0.0 : mean / s.size();
+    if (!d.opt.white) {
+      for (float v : s) mean += v;
+      mean = s.empty() ? 0.0 : mean / s.size();
+    }
     if (k == 0) rc = e0.setup(g, s, static_cast<float>(mean));
     else rc = e0.load_slot(static_cast<uint32_t>(k), s, static_cast<float>(mean));
     if (rc) return rc;

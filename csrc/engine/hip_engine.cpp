@@ -394,12 +394,6 @@ struct HipEngine::Impl {
   DevBuf<uint8_t> w_rmed;       // wide-window running-median scratch (whitening)
   DevBuf<float> ps;             // [batch][ps_stride]
   DevBuf<float> pyr;            // [batch][hs_pyr_stride(ps_stride)]: 8-bin maxima of the spectrum (pruned HS)
-  DevBuf<float> pyr1;           // the odd bins of cells pass 3 splits (p3_cells; zero elsewhere)
-  // pass 3 writes the 8-bin cell maxima of the spectrum it stores, so the
-  // harmonic sum does not re-read the spectrum for them (hs_cells_kernel).
-  // BRP_P3_CELLS=0/1; only with the three-pass FFT and direct 8-bin bounds
-  bool p3_cells = false;
-  bool cells_fused() const { return p3_cells && !bs && hs_prune && hs_cell_shift == 3 && hs_direct; }
   bool hs_prune = true;         // pruned harmonic sum (BRP_HS_FULL=1: every block exactly)
   int hs_cell_shift = 3;        // its bound cells: 8 bins (BRP_HS_CELL=4: 4 bins, tighter bounds but
                                 // 44 KB LDS / 125 VGPRs per workgroup: 16.4-16.7k vs 15.6-15.8k templates/s)
@@ -709,11 +703,6 @@ struct HipEngine::Impl {
         a3.norm = static_cast<float>(1.0 / g.nsamples);
         a3.tmpl = tmpl.p;
         a3.delta = delta.p;
-        if (cells_fused() && !select_mode) {
-          a3.cells = pyr.p;
-          a3.cells1 = pyr1.p;
-          a3.cells_stride = hipk::hs_pyr_stride(ps_stride);
-        }
         return hipk::launch_pass3(plan, hipk::P3_POWER, a3, nb, stream);
       }
       case kHarmonic: {
@@ -737,8 +726,6 @@ struct HipEngine::Impl {
         ah.pyr_stride = hipk::hs_pyr_stride(ps_stride);
         ah.key_base = key_base;
         ah.bin_bits = bin_bits;
-        ah.cells_ready = cells_fused();
-        ah.pyr1 = pyr1.p;
         if (select_mode) {
           hipk::HsSelectArgs sa{};
           sa.dense = sel_dense.p;
@@ -1049,19 +1036,6 @@ int HipEngine::setup_impl(const SearchGeometry& g, const float* host_series, con
   d.hs_direct = std::getenv("BRP_HS_DIRECT") == nullptr || std::atoi(std::getenv("BRP_HS_DIRECT")) != 0;
   d.hs_xcd = std::getenv("BRP_HS_XCD") != nullptr && std::atoi(std::getenv("BRP_HS_XCD")) == 1;
   if ((rc = d.pyr.alloc(B * hipk::hs_pyr_stride(d.ps_stride)))) return rc;
-  {
-    const char* e = std::getenv("BRP_P3_CELLS");
-    d.p3_cells = e != nullptr && std::atoi(e) != 0;
-  }
-  if (d.cells_fused()) {
-    // cells pass 3 never writes (past the limit; the odd-bin array outside
-    // split cells) must read as 0: cleared once, rewritten identically per template
-    if ((rc = d.pyr1.alloc(B * hipk::hs_pyr_stride(d.ps_stride)))) return rc;
-    BRP_HIP_CHECK(hipMemsetAsync(d.pyr.p, 0, d.pyr.n * sizeof(float), d.stream), RADPUL_HIP_MEM_COPY_HOST_DEVICE);
-    BRP_HIP_CHECK(hipMemsetAsync(d.pyr1.p, 0, d.pyr1.n * sizeof(float), d.stream), RADPUL_HIP_MEM_COPY_HOST_DEVICE);
-  } else {
-    d.pyr1.release();
-  }
   if ((rc = d.partials.alloc(B * d.plan.wg1()))) return rc;  // pass-1 partial sums (P1_RESAMPLE / P1_CHIRP*)
   if (d.bs) {
     if ((rc = d.bs_a.alloc(B * d.plan.M)) || (rc = d.bs_h.alloc(d.plan.M))) return rc;

@@ -105,14 +105,6 @@ struct Pass3Args {
   const double* delta;         // [batch] mean-padding correction (pass 2)
   // P3_COMPLEX
   float2* spec;                // fft_size complex bins
-  // P3_POWER*, optional: 8-bin maxima of the written spectrum for the pruned
-  // harmonic sum (replaces hs_cells_kernel's re-read of the spectrum). A cell
-  // whose 8 bins come from two row groups (the mirror rows of the untangle
-  // are one bin off the 8-bin grid) is split: 7 bins into `cells`, the odd bin
-  // into `cells1` (0 everywhere else); the harmonic sum reads max of both.
-  float* cells;                // [batch][cells_stride] or nullptr
-  float* cells1;               // [batch][cells_stride]
-  uint32_t cells_stride;
 };
 
 // plain row pass of the inverse transform: conj, scale, write the first

@@ -744,75 +744,6 @@ __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Arg
   // rotations: W_2N^k and W_2N^{n_s k} are stepped by one complex multiply per
   // bin (a few ulp over L / kStreams steps) instead of two table products.
   static_assert(L % kStreams == 0, "whole untangle iterations");
-  // Fused 8-bin cell maxima (Pass3Args::cells): the ROWS = 8 lanes s of one
-  // k3 stream hold bins c0 .. c0 + 7 (+ C k3): one whole cell (c0, C are
-  // multiples of 8). Their mirror bins C - c0 - s (+ C (L - 1 - k3)) are one
-  // off the grid: lanes 1..7 fill 7 bins of cell (C - c0) / 8 - 1 (`cells`),
-  // lane 0 the first bin of the next cell (`cells1`). Every cell has exactly
-  // one writer per array, so no atomics; cells past the limit are skipped.
-  static_assert(!kPower || ROWS == 8, "fused cells: one 8-bin cell per 8-lane group");
-  const bool cells = kPower && a.cells != nullptr;
-  float* const cl = cells ? a.cells + static_cast<size_t>(b) * a.cells_stride : nullptr;
-  float* const cl1 = cells ? a.cells1 + static_cast<size_t>(b) * a.cells_stride : nullptr;
-  const uint32_t nlim = (a.limit + 7) / 8;  // cells holding at least one written bin
-  auto group8_max = [](float v) {
-    v = fmaxf(v, __shfl_xor(v, 1, kWave));
-    v = fmaxf(v, __shfl_xor(v, 2, kWave));
-    return fmaxf(v, __shfl_xor(v, 4, kWave));
-  };
-  const uint32_t c0u = c0;
-  if (cells) {
-    // wave-uniform structure: every lane runs the same iterations (rows above
-    // C/2 contribute 0), so the 8-lane shuffles see all their partners
-    // twiddles stepped exactly as in the plain loop below (same powers, bit for bit)
-    float2 tk = cmul(rt.t1, w4(static_cast<uint32_t>(t)));
-    const float2 tk_step = w4(static_cast<uint32_t>(kStreams));
-    float2 ta = make_float2(0.f, 0.f), ta_step = make_float2(1.f, 0.f);
-    if (correct) {
-      ta = cmul(rt.ta, w4((n_s * static_cast<uint32_t>(t)) % L4));
-      ta_step = w4((n_s * static_cast<uint32_t>(kStreams)) % L4);
-    }
-#pragma unroll
-    for (int it = 0; it < L / kStreams; ++it) {
-      const int k3 = t + it * kStreams;
-      if (it > 0) {
-        tk = cmul(tk, tk_step);
-        if (correct) ta = cmul(ta, ta_step);
-      }
-      float vd = 0.0f, vm = 0.0f;
-      if (c <= half) {
-        const float2 zk = data[Lay::idx(k3, s)];
-        const int k3m = (c == 0) ? (L - k3) % L : L - 1 - k3;
-        const float2 zm = data[Lay::idx(k3m, c == 0 ? s : ROWS + s)];
-        const uint32_t k = c + a.C * static_cast<uint32_t>(k3);
-        const float2 w = cmul(tk, tk);
-        vd = emit(k, untangle_w(zk, zm, w), tk, ta);
-        if (c != 0 && c != half) {
-          const float2 wm = make_float2(-w.x, w.y);
-          vm = emit(a.M - k, untangle_w(zm, zk, wm), make_float2(-tk.y, -tk.x), rot_mi(conjf2(ta), n_s));
-        }
-        if (c == 0 && k3 == 0) {
-          const float vn = emit.nyquist(zk, n_s);
-          if (a.M / 8 < nlim) cl1[a.M / 8] = vn;  // bin M alone in its cell
-        }
-      }
-      const float md = group8_max(vd);
-      const float m7 = group8_max(s == 0 ? 0.0f : vm);
-      if (s == 0 && c0u <= half) {
-        const uint32_t xd = (c0u + a.C * static_cast<uint32_t>(k3)) >> 3;
-        if (xd < nlim) {
-          if (c0u < half) cl[xd] = md;
-          else cl1[xd] = md;  // row C/2 alone: the odd bin of its cell
-        }
-        if (c0u < half) {
-          const uint32_t xm = (a.C - c0u + a.C * static_cast<uint32_t>(L - 1 - k3)) >> 3;  // cell of bin C - c0
-          if (xm - 1 < nlim) cl[xm - 1] = m7;
-          if (c0u != 0 && xm < nlim) cl1[xm] = vm;
-        }
-      }
-    }
-    return;
-  }
   if (c <= half) {
     float2 tk = cmul(rt.t1, w4(static_cast<uint32_t>(t)));  // W_2N^k for k3 = t
     const float2 tk_step = w4(static_cast<uint32_t>(kStreams));

@@ -429,8 +429,8 @@ using f4u = fvu<4>;
 
 // the entries from lo of harmonic kHarm[Q] a block can reach, as one load of
 // exactly that many dwords (45 instead of 64 VGPRs for the 16 harmonics)
-template <int CK, int Q, int MODE, bool SPLIT>
-__device__ __forceinline__ f4u hs_direct_load(const PsT<MODE>* P, const float* C8, const float* C8b, int32_t ib) {
+template <int CK, int Q, int MODE>
+__device__ __forceinline__ f4u hs_direct_load(const PsT<MODE>* P, const float* C8, int32_t ib) {
   using H = HsDirect<CK, Q>;
   const uint32_t lo = hs_cell(H::L, H::K, ib);
   f4u v = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -438,16 +438,10 @@ __device__ __forceinline__ f4u hs_direct_load(const PsT<MODE>* P, const float* C
     const float* src = (H::K > 0 ? C8 : reinterpret_cast<const float*>(P)) + lo;
     if constexpr (H::kN == 1) {
       v.x = *src;
-      if constexpr (SPLIT && H::K > 0) v.x = fmaxf(v.x, C8b[lo]);
     } else {
       const fvu<H::kN> w = *reinterpret_cast<const fvu<H::kN>*>(src);
 #pragma unroll
       for (int e = 0; e < H::kN; ++e) v[e] = w[e];
-      if constexpr (SPLIT && H::K > 0) {  // cells split by pass 3: the odd bins' array
-        const fvu<H::kN> w1 = *reinterpret_cast<const fvu<H::kN>*>(C8b + lo);
-#pragma unroll
-        for (int e = 0; e < H::kN; ++e) v[e] = fmaxf(v[e], w1[e]);
-      }
     }
   } else {
 #pragma unroll
@@ -485,10 +479,10 @@ __device__ __forceinline__ void hs_direct_max(f4u v, int32_t ib, float& m16, flo
 // the ordering pins the staged path needs, the compiler waited for each pair
 // of loads in turn: ~8 memory latencies per wave); sums in the reference
 // order as in hs_bounds.
-template <int CK, int MODE, bool SPLIT, int... Q>
+template <int CK, int MODE, int... Q>
 __device__ __forceinline__ void hs_bounds_direct(std::integer_sequence<int, Q...>, const PsT<MODE>* P,
-                                                 const float* C8, const float* C8b, int32_t ib, float* u) {
-  const f4u v[16] = {hs_direct_load<CK, Q, MODE, SPLIT>(P, C8, C8b, ib)...};
+                                                 const float* C8, int32_t ib, float* u) {
+  const f4u v[16] = {hs_direct_load<CK, Q, MODE>(P, C8, ib)...};
   // every load in flight before the first is consumed (the scheduler otherwise
   // splits them into two rounds around the first maxima)
   auto issued = [](f4u x) { asm volatile("" ::"v"(x)); };
@@ -590,7 +584,7 @@ __device__ __forceinline__ void hs_bounds(std::integer_sequence<int, Q...>, cons
 // of harmonic_sum_kernel for the groups whose first index lies in the block.
 // (No global block list: an atomic per wave on one counter serialised a first
 // version at 39 us.)
-template <int CK, int MODE, bool DIRECT, bool SPLIT = false>
+template <int CK, int MODE, bool DIRECT>
 __global__ void __launch_bounds__(256) hs_pruned_kernel(HSArgs a, uint32_t nblk) {
 #pragma clang fp contract(off)
   static_assert(!DIRECT || CK == 3, "direct bound reads: 8-bin cells");
@@ -633,9 +627,7 @@ __global__ void __launch_bounds__(256) hs_pruned_kernel(HSArgs a, uint32_t nblk)
   if (blk < nblk) {
     const int32_t ib = I0 + kBlk * lane;
     float u[5];
-    if constexpr (DIRECT)
-      hs_bounds_direct<CK, MODE, SPLIT>(std::make_integer_sequence<int, 16>{}, P, C8,
-                                        SPLIT ? a.pyr1 + static_cast<size_t>(b) * a.pyr_stride : nullptr, ib, u);
+    if constexpr (DIRECT) hs_bounds_direct<CK, MODE>(std::make_integer_sequence<int, 16>{}, P, C8, ib, u);
     else hs_bounds<CK, DIRECT, MODE>(std::make_integer_sequence<int, 16>{}, buf, P, C8, I0, ib, u);
 #pragma unroll
     for (int h = 0; h <= 4; ++h) {
@@ -852,12 +844,6 @@ hipError_t launch_harmonic_sum(const HSArgs& a, int batch, hipStream_t s) {
     hipLaunchKernelGGL((hs_cells_kernel<CK, MODE>), gc, dim3(256), 0, s, a);         \
     hipLaunchKernelGGL((hs_pruned_kernel<CK, MODE, DIRECT>), gp, dim3(256), 0, s, a, nblk); \
   } while (0)
-    if (a.cells_ready) {  // pass 3 wrote the cells: direct 8-bin bounds only
-      if (a.cell_shift != 3 || !a.direct || a.pyr1 == nullptr) return hipErrorInvalidValue;
-      if (a.mode == HS_F16) hipLaunchKernelGGL((hs_pruned_kernel<3, HS_F16, true, true>), gp, dim3(256), 0, s, a, nblk);
-      else hipLaunchKernelGGL((hs_pruned_kernel<3, HS_F32, true, true>), gp, dim3(256), 0, s, a, nblk);
-      return hipGetLastError();
-    }
     if (a.mode == HS_F16) {
       if (a.cell_shift == 2) BRP_HS_PRUNED(2, HS_F16, false);
       else if (a.direct) BRP_HS_PRUNED(3, HS_F16, true);

@@ -41,10 +41,6 @@ struct HSArgs {
   uint32_t bin_bits;  // candidate key layout (hs_pack): bins < 2^bin_bits
   float* dense;       // select path: [batch][5][dense_stride] level values (HsSelectArgs)
   uint32_t dense_stride;
-  // pass 3 wrote the 8-bin cells (Pass3Args::cells): skip hs_cells_kernel; the
-  // bound reads take max(pyr, pyr1) (pyr1: the odd bins of split cells)
-  bool cells_ready;
-  const float* pyr1;
 };
 
 // cells covering the spectrum row, room for 4-bin cells (bins >= hhi count as 0)

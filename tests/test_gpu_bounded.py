@@ -71,7 +71,9 @@ def test_small_list_overflow_reruns_exactly(brp, gpu, case, tmp_path, monkeypatc
 def test_reference_wu_without_whitening_vs_cpu_golden(brp, gpu, tmp_path):
     """The shipped WU without -W (raw powers ~1.4e6: 329 049 of 329 052
     fundamental bins of template 0 exceed thr1): first 20 templates against
-    the CPU golden model (tools/make_golden.py --end 20 --no-white)."""
+    the CPU golden model (tools/make_golden.py --end 20 --no-white, which pads
+    with the accurate mean like the device: on a raw series the reference
+    CPU build's serial float mean is ~2 % off, cpu_backend.cpp)."""
     cfg = SearchConfig(inputfile=str(WU), templatebank=str(BANK), zaplistfile=str(ZAP), fA=0.08, padding=3.0,
                        f0=400.0, white=False, batch=1)
     g = BRPSearch(cfg, pipelines=3).run(begin=0, end=20, write_output=False, use_checkpoint=False)
@@ -104,19 +106,3 @@ def test_false_alarm_near_one(brp, gpu, case, tmp_path, fA):
     c = BRPSearch(_cfg(case, tmp_path / "c", fA=fA, use_cpu=True)).run(write_output=False, use_checkpoint=False)
     _compare_tables(g.table, c.table)
 
-
-def test_pass3_fused_cells_equal_cells_kernel(brp, gpu, case, tmp_path, monkeypatch):
-    """BRP_P3_CELLS=1: pass 3 writes the 8-bin cell maxima (split cells of the
-    mirror rows into two arrays) instead of hs_cells_kernel re-reading the
-    spectrum. The bounds are the same maxima, so the candidate tables are
-    byte-identical to the default path (synthetic case and the first
-    templates of the benchmark WU)."""
-    ref = _run(_cfg(case, tmp_path / "a", batch=4))
-    monkeypatch.setenv("BRP_P3_CELLS", "1")
-    fused = _run(_cfg(case, tmp_path / "b", batch=4))
-    assert bytes(fused.table.to_bytes()) == bytes(ref.table.to_bytes())
-    cfg = SearchConfig.benchmark(str(WU), str(BANK), str(ZAP), batch=1)
-    a = BRPSearch(cfg, pipelines=3).run(begin=0, end=40, write_output=False, use_checkpoint=False)
-    monkeypatch.delenv("BRP_P3_CELLS")
-    b = BRPSearch(cfg, pipelines=3).run(begin=0, end=40, write_output=False, use_checkpoint=False)
-    assert bytes(a.table.to_bytes()) == bytes(b.table.to_bytes())

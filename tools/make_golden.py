@@ -36,10 +36,14 @@ def main() -> None:
     ap.add_argument("--fA", type=float, default=0.08, help="false-alarm rate -A")
     ap.add_argument("--f0", type=float, default=400.0, help="maximum signal frequency -f")
     ap.add_argument("--padding", type=float, default=3.0, help="padding factor -P")
-    ap.add_argument("--no-white", action="store_true", help="no whitening (no -W)")
+    ap.add_argument("--no-white", action="store_true",
+                    help="no whitening (no -W); the padding mean is then taken in double precision "
+                         "(BRP_CPU_MEAN=double: the GPU / CUDA-build semantics, see cpu_backend.cpp)")
     ap.add_argument("--out", default=str(ROOT / "data" / "golden"))
     a = ap.parse_args()
     os.environ["BRP_NO_RESULT_HEADER"] = "1"
+    if a.no_white:
+        os.environ["BRP_CPU_MEAN"] = "double"
     import boinc_app_eah_brp_amd as pkg
     from boinc_app_eah_brp_amd.models import SearchConfig
 
@@ -63,7 +67,7 @@ def main() -> None:
     dt = time.time() - t0
     (out / f"bench_wu_cpu_table{suffix}.bin").write_bytes(bytes(r["table"].to_bytes()))
     meta = dict(templates=r["templates_run"], templates_total=r["templates_total"], seconds=dt, threads=a.threads,
-                flags=f"-A {a.fA:g} -P {a.padding:g} -f {a.f0:g}" + ("" if a.no_white else " -W"), backend="cpu golden (double FFT, reference float order)")
+                flags=f"-A {a.fA:g} -P {a.padding:g} -f {a.f0:g}" + (" (accurate padding mean)" if a.no_white else " -W"), backend="cpu golden (double FFT, reference float order)")
     (out / f"bench_wu_cpu_meta{suffix}.json").write_text(json.dumps(meta, indent=1) + "\n")
     print(json.dumps(meta))
 
