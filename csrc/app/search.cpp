@@ -344,12 +344,13 @@ int SearchSession::prepare() {
   SearchOptions opt0 = d.opt;
   opt0.device_series = device_all;
   const bool hip0 = std::strcmp(d.backends[0]->name(), "hip") == 0;
-  if (hip0 && !d.wu_pin) d.wu_pin = hip_pin_host(d.wu.samples.data(), d.wu.samples.size() * sizeof(float));
+  if (hip0 && !d.wu_pin && !d.wu.packed.empty())  // the payload is what crosses PCIe (setup_wu)
+    d.wu_pin = hip_pin_host(d.wu.packed.data(), d.wu.packed.size());
   // a HIP backend that keeps the whitened series on the device only reads
   // the raw samples: upload them straight from the (page-locked) WU buffer
   const bool direct = hip0 && device_all;
   if (!direct) d.series = d.wu.samples;
-  int rc = d.backends[0]->setup(d.g, opt0, direct ? d.wu.samples : d.series, d.zaps);
+  int rc = direct ? d.backends[0]->setup_wu(d.g, opt0, d.wu, d.zaps) : d.backends[0]->setup(d.g, opt0, d.series, d.zaps);
   if (rc) {
     boinc::end_critical_section();
     return rc;

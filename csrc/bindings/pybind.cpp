@@ -429,6 +429,18 @@ PYBIND11_MODULE(_brp, m) {
              std::vector<float> v(series.data(), series.data() + series.size());
              check(e.setup(dict_to_geometry(gd), v, mu0), "HipEngine.setup");
            })
+      .def("setup_from_wu",
+           [](HipEngine& e, const py::dict& gd, const std::string& path, float mu0) {
+             WorkUnit wu;
+             check(read_work_unit(path, wu), "read_work_unit");
+             check(e.setup_packed(dict_to_geometry(gd), wu, mu0), "HipEngine.setup_packed");
+           })
+      .def("download_series",
+           [](HipEngine& e) {
+             std::vector<float> v;
+             check(e.download_series(v), "HipEngine.download_series");
+             return py::array_t<float>(v.size(), v.data());
+           })
       .def("whiten",
            [](HipEngine& e, const py::dict& od, std::vector<std::pair<double, double>> zaps,
               py::array_t<float, py::array::c_style> series) {

@@ -56,6 +56,7 @@ int read_work_unit(const std::string& path, WorkUnit& wu) {
   }
   const double scale = wu.header.scale;
   wu.samples.assign(n, 0.0f);
+  wu.packed = packed;
   if (wu.four_bit) {
     for (uint32_t i = 0; i < n_packed; ++i) {
       const uint8_t c = packed[i];

@@ -15,6 +15,10 @@ struct WorkUnit {
   DDHeader header{};           // byte-swapped to host order
   bool four_bit = true;        // .bin4 (4-bit) or .binary (8-bit)
   std::vector<float> samples;  // header.nsamples unpacked samples
+  // the payload as stored (2 samples per byte for 4-bit): a device uploads
+  // these n/2 (or n) bytes and unpacks them itself (hipk::launch_unpack)
+  // instead of the 4n bytes of floats
+  std::vector<uint8_t> packed;
 };
 
 // Format from the file name: ".binary" -> 8-bit, ".bin4" -> 4-bit, else

@@ -50,6 +50,12 @@ class Backend {
   // updated in place with the whitened data).
   virtual int setup(const SearchGeometry& g, const SearchOptions& opt, std::vector<float>& series,
                     const std::vector<ZapRange>& zaps) = 0;
+  // the same from the whole work unit (series = wu.samples): a device backend
+  // may upload the stored payload and unpack it itself
+  virtual int setup_wu(const SearchGeometry& g, const SearchOptions& opt, WorkUnit& wu,
+                       const std::vector<ZapRange>& zaps) {
+    return setup(g, opt, wu.samples, zaps);
+  }
   // Process n templates with device thresholds thr (<= the sequential
   // thresholds of every template in the batch).
   virtual int process(const TemplateInput* t, int n, const float thr[kNumHarmonicLevels],

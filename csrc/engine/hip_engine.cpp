@@ -313,6 +313,7 @@ struct HipEngine::Impl {
   // per submitted batch instead of one per group (an event record costs the
   // stream ~7 us of idle GPU time; profiles/README.md round 3). BRP_SERIAL.
   int serial = 1;
+  int batch_req = 4, serial_req = 1;  // as requested at init (setup adapts them to the geometry)
   int slot_cap() const { return batch * serial; }  // templates per submitted batch
   hipEvent_t prev_done = nullptr;  // completion event of the last completed batch (device-time statistics)
   uint32_t key_base = 0;        // template index of the current launch group within its batch
@@ -348,6 +349,10 @@ struct HipEngine::Impl {
   // then the length-L plan of the convolution, the DFT has length bs_Mb
   // (N/2 for even N, N for odd N); bluestein_kernels.hpp
   bool bs = false;
+  // odd N: two templates per chirp-z transform (real / imaginary part,
+  // P1_CHIRP1_PAIR), half the convolution work per template. BRP_BS_PAIR=0: one
+  bool bs_pair = false;
+  int bs_trans(int nb) const { return bs_pair ? (nb + 1) / 2 : nb; }
   uint32_t bs_Mb = 0;
   DevBuf<float2> bs_a;          // [batch][L] chirp-in / convolution spectrum / A
   DevBuf<float2> bs_h;          // [L] FFT_L of the wrapped conjugate chirp
@@ -365,6 +370,7 @@ struct HipEngine::Impl {
   bool fg_in = false, fg_out = false;
 
   DevBuf<float> series;
+  DevBuf<uint8_t> wu_packed;    // staging of the WU payload (setup_packed)
   // read-only series of a sibling pipeline on the same device (adopt_series):
   // one copy for all pipelines keeps the Infinity-Cache footprint down
   const float* shared_series = nullptr;
@@ -453,6 +459,26 @@ struct HipEngine::Impl {
   DevBuf<float> w_psw, w_med;   // whitening scratch: power spectrum, running median
   DevBuf<uint32_t> w_zbins;     // whitening: zapped bins and their noise
   DevBuf<float2> w_znoise;
+  // Whitening that keeps its result on the device returns without waiting:
+  // the pipelines that read the series order themselves after it with
+  // ev_w1 (adopt_series), so the host's prepare / launch work overlaps the
+  // whitening kernels. The host noise arrays stay alive until ev_w1 has passed.
+  std::vector<float2> w_zn_host;
+  std::vector<uint32_t> w_zb_host;
+  hipEvent_t ev_w0 = nullptr, ev_w1 = nullptr, ev_adopt = nullptr;
+  bool w_pending = false;       // ev_w0 / ev_w1 of an asynchronous whitening not yet accounted
+  // whitening device time of a finished asynchronous whitening into the stats
+  void settle_whiten(bool wait) {
+    if (!w_pending) return;
+    if (!wait && hipEventQuery(ev_w1) != hipSuccess) {
+      (void)hipGetLastError();
+      return;
+    }
+    (void)hipEventSynchronize(ev_w1);
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, ev_w0, ev_w1) == hipSuccess) st.whiten_ms += ms;
+    w_pending = false;
+  }
   DevBuf<float2> t_st1, t_st2, t_st3, t_p1, t_p2col, t_p2lo, t_p2hi, t_p3;
 
   struct { TemplateDev* p = nullptr; } h_tmpl;
@@ -535,7 +561,8 @@ struct HipEngine::Impl {
   }
   // passes 2 and 3 of a length-L transform in buf; n_partials > 0: pass 2
   // also reduces pass 1's template partial sums (delta)
-  hipError_t bs_fft_rest(int nb, hipk::Pass3CplxMode mode, float2* out, uint32_t n_partials) {
+  hipError_t bs_fft_rest(int nb, hipk::Pass3CplxMode mode, float2* out, uint32_t n_partials, uint32_t tpt = 1,
+                         uint32_t n_tmpl = 0) {
     const hipk::TwiddleTable tw = twt();
     const bool reduce_delta = n_partials > 0;
     hipError_t e;
@@ -551,6 +578,8 @@ struct HipEngine::Impl {
       a2.n_partials = n_partials;
       a2.tmpl = tmpl.p;
       a2.delta = delta.p;
+      a2.tpt = tpt;
+      a2.n_tmpl = n_tmpl;
     }
     if ((e = hipk::launch_pass2(plan, a2, nb, stream)) != hipSuccess) return e;
     hipk::Pass3CplxArgs a3{};
@@ -584,10 +613,11 @@ struct HipEngine::Impl {
     a.chirp = chirpt();
     return a;
   }
-  // template spectra of a batch: pass 1 of the first convolution transform
-  // straight from the series (resampling, centring, chirp: P1_CHIRP*), its
-  // passes 2 and 3 (* H), the second transform, the power spectrum (bins
-  // k < limit into ps_out [nb][stride])
+  // template spectra of a batch of nb templates: pass 1 of the first
+  // convolution transform straight from the series (resampling, centring,
+  // chirp: P1_CHIRP*), its passes 2 and 3 (* H), the second transform, the
+  // power spectrum (bins k < limit into ps_out [nb][stride]); bs_trans(nb)
+  // transforms (paired templates for odd N)
   hipError_t bs_template_in(int nb, uint32_t* reset) {
     hipk::Pass1Args a1{};
     a1.out = buf.p;
@@ -602,9 +632,13 @@ struct HipEngine::Impl {
     a1.reset = reset;
     a1.chirp = chirpt();
     a1.Mb = bs_Mb;
-    return hipk::launch_pass1(plan, bs_Mb == g.nsamples ? hipk::P1_CHIRP1 : hipk::P1_CHIRP2, a1, nb, stream);
+    a1.n_tmpl = static_cast<uint32_t>(nb);
+    const hipk::Pass1Mode m = bs_pair ? hipk::P1_CHIRP1_PAIR : (bs_Mb == g.nsamples ? hipk::P1_CHIRP1 : hipk::P1_CHIRP2);
+    return hipk::launch_pass1(plan, m, a1, bs_trans(nb), stream);
   }
-  hipError_t bs_template_round0(int nb) { return bs_fft_rest(nb, hipk::C3_MULCONJ, bs_a.p, plan.wg1()); }
+  hipError_t bs_template_round0(int nb) {
+    return bs_fft_rest(bs_trans(nb), hipk::C3_MULCONJ, bs_a.p, plan.wg1(), bs_pair ? 2u : 1u, static_cast<uint32_t>(nb));
+  }
   hipError_t bs_template_power(int nb, float* ps_out, _Float16* ps16_out, uint32_t stride, uint32_t limit) {
     hipk::BsPowerArgs ap{};
     ap.A = bs_a.p;
@@ -619,17 +653,21 @@ struct HipEngine::Impl {
     ap.norm = static_cast<float>(1.0 / g.nsamples);
     ap.tmpl = tmpl.p;
     ap.delta = delta.p;
-    return hipk::launch_bs_power(ap, nb, stream);
+    ap.pair = bs_pair;
+    ap.n_tmpl = static_cast<uint32_t>(nb);
+    return hipk::launch_bs_power(ap, bs_trans(nb), stream);
   }
   hipError_t bs_template_spectra(int nb, float* ps_out, _Float16* ps16_out, uint32_t stride, uint32_t limit) {
     hipError_t e = bs_template_in(nb, nullptr);
     if (e == hipSuccess) e = bs_template_round0(nb);
-    if (e == hipSuccess) e = bs_round(nb, 1);
+    if (e == hipSuccess) e = bs_round(bs_trans(nb), 1);
     return e == hipSuccess ? bs_template_power(nb, ps_out, ps16_out, stride, limit) : e;
   }
 
   ~Impl() {
     bump_series();  // readers of this series must not launch any more
+    for (hipEvent_t e : {ev_w0, ev_w1, ev_adopt})
+      if (e) (void)hipEventDestroy(e);
     for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second);
     for (BatchIO& o : io) {
       if (o.ev0) (void)hipEventDestroy(o.ev0);
@@ -682,7 +720,7 @@ struct HipEngine::Impl {
       }
       case kPass3: {
         if (bs) {
-          const hipError_t e3 = bs_round(nb, 1);
+          const hipError_t e3 = bs_round(bs_trans(nb), 1);
           if (e3 != hipSuccess) return e3;
           return bs_template_power(nb, ps.p, ps_fp16 ? reinterpret_cast<_Float16*>(ps.p) : nullptr, ps_stride,
                                    std::min(g.harmonic_idx_hi, g.fft_size));
@@ -901,11 +939,16 @@ int HipEngine::init(int device, int batch) {
     const int sv = e ? std::atoi(e) : kDefaultSerial;
     impl_->serial = std::max(1, std::min(sv, static_cast<int>(hipk::kHsMaxBatch) / impl_->batch));
   }
+  impl_->batch_req = impl_->batch;
+  impl_->serial_req = impl_->serial;
   BRP_HIP_CHECK(hipStreamCreateWithFlags(&impl_->stream, hipStreamNonBlocking), RADPUL_HIP_DEVICE_SET);
   for (auto& o : impl_->io) {
     BRP_HIP_CHECK(hipEventCreate(&o.ev0), RADPUL_HIP_DEVICE_SET);
     BRP_HIP_CHECK(hipEventCreate(&o.ev1), RADPUL_HIP_DEVICE_SET);
   }
+  BRP_HIP_CHECK(hipEventCreate(&impl_->ev_w0), RADPUL_HIP_DEVICE_SET);
+  BRP_HIP_CHECK(hipEventCreate(&impl_->ev_w1), RADPUL_HIP_DEVICE_SET);
+  BRP_HIP_CHECK(hipEventCreateWithFlags(&impl_->ev_adopt, hipEventDisableTiming), RADPUL_HIP_DEVICE_SET);
   impl_->select_io(0);
   hipDeviceProp_t prop;
   BRP_HIP_CHECK(hipGetDeviceProperties(&prop, device), RADPUL_HIP_DEVICE_PROP);
@@ -929,6 +972,11 @@ int HipEngine::setup(const SearchGeometry& g, const std::vector<float>& series, 
   return setup_impl(g, series.data(), nullptr, -1, mu0);
 }
 
+int HipEngine::setup_packed(const SearchGeometry& g, const WorkUnit& wu, float mu0) {
+  if (wu.samples.size() < g.n_unpadded || wu.packed.empty()) return RADPUL_EVAL;
+  return setup_impl(g, wu.samples.data(), nullptr, -1, mu0, &wu);
+}
+
 int HipEngine::setup_peer(const HipEngine& src) {
   const Impl& s = *src.impl_;
   if (!s.ready || s.slots != 1) return RADPUL_EVAL;
@@ -938,9 +986,23 @@ int HipEngine::setup_peer(const HipEngine& src) {
   return setup_impl(s.g, nullptr, s.series_in(), s.device, s.mu0s[0]);
 }
 
-int HipEngine::upload_series0(const float* host, const float* dev_src, int src_device) {
+int HipEngine::upload_series0(const float* host, const float* dev_src, int src_device, const WorkUnit* packed) {
   Impl& d = *impl_;
   const size_t bytes = d.g.n_unpadded * sizeof(float);
+  if (packed != nullptr) {
+    // the payload (n/2 bytes for 4-bit: 2 MB instead of 16.8 MB on the
+    // benchmark WU), unpacked on the device into slot 0
+    trace::Range up("brp:series_upload_packed");
+    const size_t nb = packed->packed.size();
+    int rc;
+    if (d.wu_packed.n < nb && (rc = d.wu_packed.alloc(nb))) return rc;
+    BRP_HIP_CHECK(hipMemcpyAsync(d.wu_packed.p, packed->packed.data(), nb, hipMemcpyHostToDevice, d.stream),
+                  RADPUL_HIP_MEM_COPY_HOST_DEVICE);
+    BRP_HIP_CHECK(hipk::launch_unpack(d.wu_packed.p, static_cast<uint32_t>(nb), packed->four_bit, packed->header.scale,
+                                      d.series.p, d.g.n_unpadded, d.stream),
+                  RADPUL_HIP_KERNEL_INVOKE);
+    return 0;  // stream-ordered before everything that reads the series (the WU payload outlives the copy)
+  }
   if (dev_src != nullptr) {
     // device to device: same device, or a peer over xGMI (no host round trip)
     trace::Range up("brp:series_peer_copy");
@@ -956,7 +1018,7 @@ int HipEngine::upload_series0(const float* host, const float* dev_src, int src_d
 }
 
 int HipEngine::setup_impl(const SearchGeometry& g, const float* host_series, const float* dev_series, int src_device,
-                          float mu0) {
+                          float mu0, const WorkUnit* packed) {
   trace::Range range("brp:engine_setup");
   Impl& d = *impl_;
   BRP_HIP_CHECK(hipSetDevice(d.device), RADPUL_HIP_DEVICE_SET);
@@ -967,7 +1029,7 @@ int HipEngine::setup_impl(const SearchGeometry& g, const float* host_series, con
     d.g = g;
     d.mu0s.assign(d.slots, 0.0f);
     d.mu0s[0] = mu0;
-    return upload_series0(host_series, dev_series, src_device);
+    return upload_series0(host_series, dev_series, src_device, packed);
   }
   d.ready = false;
   for (auto& kv : d.graphs) (void)hipGraphExecDestroy(kv.second);
@@ -976,10 +1038,19 @@ int HipEngine::setup_impl(const SearchGeometry& g, const float* host_series, con
   d.mu0s.assign(d.slots, 0.0f);
   d.mu0s[0] = mu0;
   d.bs = g.nsamples % 2 != 0 || !make_fft_plan(g.nsamples / 2, d.plan);
+  d.bs_pair = false;
+  d.batch = d.batch_req;
+  d.serial = d.serial_req;
   if (d.bs) {
     // any other length (every padding -P the reference accepts): chirp-z
     // transform over the smallest factorable convolution length
     d.bs_Mb = (g.nsamples % 2) ? g.nsamples : g.nsamples / 2;
+    d.bs_pair = (g.nsamples % 2) != 0 &&
+                (std::getenv("BRP_BS_PAIR") == nullptr || std::atoi(std::getenv("BRP_BS_PAIR")) != 0);
+    if (d.bs_pair && d.batch == 1) {  // launch groups of two templates: one transform each
+      d.batch = 2;
+      d.serial = std::max(1, d.serial / 2);
+    }
     if (!make_bluestein_plan(d.bs_Mb, d.plan)) {
       log_message(LOG_ERROR, true, "No FFT plan for length %u.\n", g.nsamples);
       return RADPUL_HIP_FFT_PLAN;
@@ -1016,7 +1087,10 @@ int HipEngine::setup_impl(const SearchGeometry& g, const float* host_series, con
   }
   d.dense_stride = std::max<uint32_t>((g.fundamental_idx_hi + 63) / 64 * 64, 64);
   if (const char* e = std::getenv("BRP_HS_CAP")) {
-    d.cap = std::max<uint32_t>(64u, static_cast<uint32_t>(std::atol(e)));
+    // fault injection (small lists overflow early); never below what the
+    // bounded output of a full batch emits (100 per template and level, +28 % for ties)
+    const uint32_t min_cap = static_cast<uint32_t>(d.slot_cap()) * kNumHarmonicLevels * 128u;
+    d.cap = std::max<uint32_t>(min_cap, static_cast<uint32_t>(std::atol(e)));
     d.kcopy = std::min(d.kcopy, d.cap);
     d.inplace_max = std::min(d.inplace_max, d.kcopy);
   }
@@ -1107,7 +1181,7 @@ int HipEngine::setup_impl(const SearchGeometry& g, const float* host_series, con
     BRP_HIP_CHECK(d.bs_make_h(), RADPUL_HIP_KERNEL_INVOKE);
     BRP_HIP_CHECK(hipStreamSynchronize(d.stream), RADPUL_HIP_KERNEL_INVOKE);
   }
-  if ((rc = upload_series0(host_series, dev_series, src_device))) return rc;
+  if ((rc = upload_series0(host_series, dev_series, src_device, packed))) return rc;
   log_mem_status(d.device, "after setup");
   d.ready = true;
   return 0;
@@ -1126,7 +1200,10 @@ int HipEngine::adopt_series(const HipEngine& src) {
   d.g = s.g;
   d.mu0s = s.mu0s;
   static const bool share = std::getenv("BRP_SHARE_SERIES") == nullptr || std::atoi(std::getenv("BRP_SHARE_SERIES")) != 0;
-  BRP_HIP_CHECK(hipStreamSynchronize(s.stream), RADPUL_HIP_MEM_COPY_HOST_DEVICE);
+  // everything queued on the source's stream so far (upload, whitening) comes
+  // before this pipeline's next work: a device-side dependency, no host wait
+  BRP_HIP_CHECK(hipEventRecord(d.ev_adopt, s.stream), RADPUL_HIP_MEM_COPY_HOST_DEVICE);
+  BRP_HIP_CHECK(hipStreamWaitEvent(d.stream, d.ev_adopt, 0), RADPUL_HIP_MEM_COPY_HOST_DEVICE);
   const float* want = share ? s.series_in() : nullptr;
   if (want != d.shared_series) {
     d.shared_series = want;
@@ -1196,7 +1273,9 @@ int HipEngine::whiten(const SearchOptions& opt, const std::vector<ZapRange>& zap
   d.own_series();
   float* slot_series = d.series.p + static_cast<size_t>(slot) * d.g.n_unpadded;
   const SearchGeometry& g = d.g;
+  d.settle_whiten(true);  // the previous whitening's host noise arrays are free again
   auto t0 = std::chrono::steady_clock::now();
+  BRP_HIP_CHECK(hipEventRecord(d.ev_w0, d.stream), RADPUL_HIP_KERNEL_INVOKE);
   int32_t seed;
   std::memcpy(&seed, series.data(), sizeof(seed));
   log_message(LOG_INFO, true, "Seed for random number generator is %d.\n", seed);
@@ -1276,10 +1355,12 @@ int HipEngine::whiten(const SearchOptions& opt, const std::vector<ZapRange>& zap
   DevBuf<uint32_t>& zbins = d.w_zbins;
   DevBuf<float2>& znoise = d.w_znoise;
   const uint32_t nz = static_cast<uint32_t>(noise.bin.size());
-  // host sources of the async copies must outlive them: kept until the final
-  // stream synchronisation of this function
-  std::vector<float2> zn;
-  std::vector<uint32_t> zb;
+  // host sources of the async copies must outlive them: engine members,
+  // reused only once this whitening's end event has passed (settle_whiten)
+  std::vector<float2>& zn = d.w_zn_host;
+  std::vector<uint32_t>& zb = d.w_zb_host;
+  zn.clear();
+  zb.clear();
   if (nz) {
     // overlapping zap ranges hit a bin more than once: sequentially the last
     // draw wins, so keep only that one (the device writes bins in parallel)
@@ -1351,15 +1432,21 @@ int HipEngine::whiten(const SearchOptions& opt, const std::vector<ZapRange>& zap
     ap.n_out = g.n_unpadded;
     BRP_HIP_CHECK(hipk::launch_pass3_plain(d.plan, ap, s), RADPUL_HIP_KERNEL_INVOKE);
   }
-  if (copy_back)
+  d.mu0s[slot] = 0.0f;  // whitened series has its DC (and first window_2 bins) removed
+  if (copy_back) {
     BRP_HIP_CHECK(hipMemcpyAsync(series.data(), slot_series, g.n_unpadded * sizeof(float), hipMemcpyDeviceToHost, s),
                   RADPUL_HIP_MEM_COPY_DEVICE_HOST);
-  {
-    trace::Range wait("brp:whiten_wait");
-    BRP_HIP_CHECK(hipStreamSynchronize(s), RADPUL_HIP_KERNEL_INVOKE);
+    {
+      trace::Range wait("brp:whiten_wait");
+      BRP_HIP_CHECK(hipStreamSynchronize(s), RADPUL_HIP_KERNEL_INVOKE);
+    }
+    d.st.whiten_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return 0;
   }
-  d.mu0s[slot] = 0.0f;  // whitened series has its DC (and first window_2 bins) removed
-  d.st.whiten_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  // the series stays on the device: the templates (this stream, or streams
+  // ordered after it by adopt_series) run after the whitening without a host wait
+  BRP_HIP_CHECK(hipEventRecord(d.ev_w1, s), RADPUL_HIP_KERNEL_INVOKE);
+  d.w_pending = true;
   return 0;
 }
 
@@ -1704,7 +1791,10 @@ int HipEngine::bound_cells(int k, std::vector<float>& cells) {
   return 0;
 }
 
-BackendStats HipEngine::stats() const { return impl_->st; }
+BackendStats HipEngine::stats() const {
+  impl_->settle_whiten(false);
+  return impl_->st;
+}
 int HipEngine::device() const { return impl_->device; }
 const FFTPlan3& HipEngine::plan() const { return impl_->plan; }
 int HipEngine::batch() const { return impl_->slot_cap(); }
@@ -1730,9 +1820,18 @@ class HipBackend final : public Backend {
       return RADPUL_EVAL;
     }
     eng_.set_ps_fp16(opt.ps_fp16);
-    int rc = eng_.setup(g, series, static_cast<float>(mean));
+    int rc = packed_ != nullptr ? eng_.setup_packed(g, *packed_, static_cast<float>(mean))
+                                : eng_.setup(g, series, static_cast<float>(mean));
     if (rc == 0 && opt.white) rc = eng_.whiten(opt, zaps, series, 0, !opt.device_series);
     log_message(LOG_DEBUG, true, "HIP device allocations so far: %ld\n", g_device_allocs.load());
+    return rc;
+  }
+  int setup_wu(const SearchGeometry& g, const SearchOptions& opt, WorkUnit& wu,
+               const std::vector<ZapRange>& zaps) override {
+    // the series stays on the device (or is read back by whiten): upload the payload
+    if (!wu.packed.empty() && (opt.white ? opt.device_series : true)) packed_ = &wu;
+    const int rc = setup(g, opt, wu.samples, zaps);
+    packed_ = nullptr;
     return rc;
   }
   int process(const TemplateInput* t, int n, const float thr[kNumHarmonicLevels],
@@ -1781,6 +1880,7 @@ class HipBackend final : public Backend {
 
  private:
   HipEngine eng_;
+  const WorkUnit* packed_ = nullptr;  // setup_wu in progress
 };
 }  // namespace
 

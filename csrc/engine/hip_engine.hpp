@@ -21,6 +21,9 @@ class HipEngine {
   // allocate per-WU buffers, upload the series; mu0 = reference level
   // subtracted before the FFT (keeps the padding correction well conditioned)
   int setup(const SearchGeometry& g, const std::vector<float>& series, float mu0);
+  // the same from the WU's stored payload (WorkUnit::packed): n/2 bytes cross
+  // PCIe instead of 4n and the device unpacks them (bit-identical floats)
+  int setup_packed(const SearchGeometry& g, const WorkUnit& wu, float mu0);
   int upload_series(const std::vector<float>& series, float mu0);
   // Re-setup for the next pass over the same geometry from `src`'s (whitened)
   // series: `src` and this engine share a device, have the same number of WU
@@ -80,8 +83,8 @@ class HipEngine {
 
  private:
   int setup_impl(const SearchGeometry& g, const float* host_series, const float* dev_series, int src_device,
-                 float mu0);
-  int upload_series0(const float* host, const float* dev_src, int src_device);
+                 float mu0, const WorkUnit* packed = nullptr);
+  int upload_series0(const float* host, const float* dev_src, int src_device, const WorkUnit* packed = nullptr);
   struct Impl;
   Impl* impl_;
 };

@@ -72,27 +72,43 @@ __device__ __forceinline__ float2 bs_bin(const float2* A, uint32_t Mb, uint32_t 
 
 template <bool HALF>
 __global__ void __launch_bounds__(kThreads) bs_power_kernel(BsPowerArgs a) {
-  const int b = blockIdx.y;
+  const int b = blockIdx.y;  // transform
   const uint32_t k = blockIdx.x * kThreads + threadIdx.x;
   if (k >= a.limit) return;
-  float p = 0.0f;
   const uint32_t real_bins = a.nsamples / 2 + 1;  // bins the real DFT defines
-  if (k > 0 && k < real_bins) {
-    const float2* A = a.A + static_cast<size_t>(b) * a.L;
-    float2 x = bs_bin(A, a.Mb, a.nsamples, a.tw, k);
-    const uint32_t n_s = a.tmpl[b].n_steps;
-    if (n_s > 0) {  // + delta * S_k, S_k the transform of the padding indicator
-      const float dS = static_cast<float>(a.delta[b]);
+  const bool live = k > 0 && k < real_bins;
+  const float2* A = a.A + static_cast<size_t>(b) * a.L;
+  // X_k (+ delta * S_k, S_k the transform of the padding indicator) -> |.|^2 / N
+  auto power = [&](float2 x, uint32_t t) {
+    const uint32_t n_s = a.tmpl[t].n_steps;
+    if (n_s > 0) {
+      const float dS = static_cast<float>(a.delta[t]);
       const float2 tk = tw_lookup(a.tw, k);
       const float2 ta = tw_lookup(a.tw, static_cast<uint64_t>(n_s) * k);
       const float2 sp = padding_spectrum_t(ta, tk, cmul(ta, conjf2(tk)));  // tc = W_2N^{(n_s - 1) k}
       x = make_float2(x.x + dS * sp.x, x.y + dS * sp.y);
     }
-    p = (x.x * x.x + x.y * x.y) * a.norm;
+    return (x.x * x.x + x.y * x.y) * a.norm;
+  };
+  auto store = [&](uint32_t t, float p) {
+    const size_t o = static_cast<size_t>(t) * a.ps_stride + k;
+    if (HALF) a.ps16[o] = static_cast<_Float16>(fminf(p, 65504.0f));  // saturate: no inf in the fp16 spectrum
+    else a.ps[o] = p;
+  };
+  if (!a.pair) {
+    store(b, live ? power(bs_bin(A, a.Mb, a.nsamples, a.tw, k), b) : 0.0f);
+    return;
   }
-  const size_t o = static_cast<size_t>(b) * a.ps_stride + k;
-  if (HALF) a.ps16[o] = static_cast<_Float16>(fminf(p, 65504.0f));  // saturate: no inf in the fp16 spectrum
-  else a.ps[o] = p;
+  // odd N, A = DFT of x_a + i x_b: X_a = (A_k + conj A_{N-k}) / 2, X_b = -i (A_k - conj A_{N-k}) / 2
+  const uint32_t ta = 2 * b, tb = 2 * b + 1;
+  float pa = 0.0f, pb = 0.0f;
+  if (live) {
+    const float2 ak = A[k], am = conjf2(A[a.nsamples - k]);
+    pa = power(make_float2(0.5f * (ak.x + am.x), 0.5f * (ak.y + am.y)), ta);
+    if (tb < a.n_tmpl) pb = power(make_float2(0.5f * (ak.y - am.y), -0.5f * (ak.x - am.x)), tb);
+  }
+  store(ta, pa);
+  if (tb < a.n_tmpl) store(tb, pb);
 }
 
 __global__ void __launch_bounds__(kThreads) bs_spec_kernel(const float2* A, uint32_t Mb, uint32_t N, TwiddleTable tw,

@@ -80,6 +80,10 @@ struct BsPowerArgs {
   float norm;                  // 1/N
   const TemplateDev* tmpl;
   const double* delta;         // [batch] mean of the centred samples (pass 2 of the first FFT)
+  // paired odd-N transforms (P1_CHIRP1_PAIR): transform p holds templates 2p
+  // (real part) and 2p + 1 (imaginary part, < n_tmpl); A is [transform][L]
+  bool pair;
+  uint32_t n_tmpl;
 };
 
 hipError_t launch_bs_chirp_in(BsInMode mode, const BsInArgs& a, int batch, uint32_t* n_partials, hipStream_t s);

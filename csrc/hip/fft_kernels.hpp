@@ -46,6 +46,10 @@ enum Pass1Mode : int {
   // the series (the chirp-multiplied input is never materialised)
   P1_CHIRP2 = 4,        // even N: (x[2n], x[2n+1]) w_n
   P1_CHIRP1 = 5,        // odd N: x[n] w_n
+  // odd N, two templates per transform: (x_a[n] + i x_b[n]) w_n for templates
+  // 2p and 2p + 1 of the launch (X_a, X_b separate by conjugate symmetry in
+  // bs_power_kernel): half the chirp-z work per template
+  P1_CHIRP1_PAIR = 6,
 };
 
 struct Pass1Args {
@@ -67,6 +71,7 @@ struct Pass1Args {
   // P1_CHIRP*: chirp W_{2 Mb}^{n^2} of the length-Mb DFT (also uses series/tmpl/partials)
   TwiddleTable chirp;
   uint32_t Mb;
+  uint32_t n_tmpl;             // P1_CHIRP1_PAIR: templates of the launch (transform p: 2p, 2p + 1 < n_tmpl)
 };
 
 struct Pass2Args {
@@ -81,6 +86,10 @@ struct Pass2Args {
   uint32_t n_partials;
   const TemplateDev* tmpl;
   double* delta;               // [batch]
+  // templates per transform (2: paired chirp-z transforms, P1_CHIRP1_PAIR;
+  // 0 counts as 1) and templates of the launch: transform p reduces the
+  // partial sums of templates tpt p .. tpt p + tpt - 1 (< n_tmpl)
+  uint32_t tpt, n_tmpl;
 };
 
 enum Pass3Mode : int {

@@ -50,7 +50,7 @@ __global__ void __launch_bounds__(kNcol * tpc_for<L>()) pass1_kernel(Pass1Args a
   Lay::coords(threadIdx.x, c, tj);
   if (a.reset != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *a.reset = 0;
 
-  double sum = 0.0;
+  double sum = 0.0, sum_b = 0.0;  // sum_b: the second template of a pair (P1_CHIRP1_PAIR)
   bool pruned = false;
   if (MODE == P1_RESAMPLE) {
     __shared__ float lut_s[kLutSize], lut_c[kLutSize];
@@ -112,41 +112,55 @@ __global__ void __launch_bounds__(kNcol * tpc_for<L>()) pass1_kernel(Pass1Args a
     const float fsum = pruned ? gather(std::integral_constant<int, kPerPruned>{})
                               : gather(std::integral_constant<int, kPer>{});
     sum = static_cast<double>(fsum);
-  } else if (MODE == P1_CHIRP2 || MODE == P1_CHIRP1) {
+  } else if (MODE == P1_CHIRP2 || MODE == P1_CHIRP1 || MODE == P1_CHIRP1_PAIR) {
     __shared__ float lut_s[kLutSize], lut_c[kLutSize];
     for (int i = threadIdx.x; i < kLutSize; i += NT) {
       lut_s[i] = kSinLut[i];
       lut_c[i] = kCosLut[i];
     }
     __syncthreads();
+    constexpr bool kPair = MODE == P1_CHIRP1_PAIR;
     const bool fast = a.n_unpadded <= (1u << 23);
-    const TemplateDev td = a.tmpl[b];
+    const int ta = kPair ? 2 * b : b;
+    const bool has_b = kPair && static_cast<uint32_t>(ta + 1) < a.n_tmpl;
+    const TemplateDev td = a.tmpl[ta];
+    TemplateDev tdb = td;
+    if (has_b) tdb = a.tmpl[ta + 1];
     const float* series = a.series + static_cast<size_t>(td.wu) * a.n_unpadded;
+    const float* series_b = a.series + static_cast<size_t>(tdb.wu) * a.n_unpadded;
     const int last = static_cast<int>(a.n_unpadded) - 1;
     // the convolution input is zero from Mb on (L >= 2 Mb - 1): with
     // Mb <= (L / R0) L2L3 the rows n1 >= L / R0 are all zero (run_pruned)
     constexpr int kR0 = BlockFFT<L, kNcol, TPC, false>::kFirstRadix;
     pruned = static_cast<uint64_t>(L / kR0) * a.L2L3 >= a.Mb;
     const int rows_valid = pruned ? L / kR0 : L;
-    auto sample = [&](uint32_t m) -> float {
-      if (m >= td.n_steps) return 0.0f;
-      const float dt = resamp_del_t(m, td.p, lut_s, lut_c);
+    auto sample_of = [&](const TemplateDev& t, const float* ser, uint32_t m) -> float {
+      if (m >= t.n_steps) return 0.0f;
+      const float dt = resamp_del_t(m, t.p, lut_s, lut_c);
       const int i = min(max(fast ? resamp_nearest_f(m, dt) : resamp_nearest(m, dt), 0), last);
-      return series[i] - td.mu0;
+      return ser[i] - t.mu0;
     };
-    float fsum = 0.0f;
+    auto sample = [&](uint32_t m) { return sample_of(td, series, m); };
+    float fsum = 0.0f, fsum_b = 0.0f;
     for (int r = tj; r < rows_valid; r += TPC) {
       const uint32_t n = r * a.L2L3 + col_base + c;
       float2 v = make_float2(0.0f, 0.0f);
       if (n < a.Mb) {
-        const float2 x = MODE == P1_CHIRP2 ? make_float2(sample(2 * n), sample(2 * n + 1))
-                                           : make_float2(sample(n), 0.0f);
-        fsum += x.x + x.y;
+        float2 x;
+        if (MODE == P1_CHIRP2) {
+          x = make_float2(sample(2 * n), sample(2 * n + 1));
+          fsum += x.x + x.y;
+        } else {
+          x = make_float2(sample(n), has_b ? sample_of(tdb, series_b, n) : 0.0f);
+          fsum += x.x;
+          fsum_b += x.y;
+        }
         v = cmul(x, tw_lookup(a.chirp, static_cast<uint64_t>(n) * n));  // W_{2Mb}^{n^2 mod 2Mb}
       }
       data[Lay::idx(r, c)] = v;
     }
     sum = static_cast<double>(fsum);
+    sum_b = static_cast<double>(fsum_b);
   } else if (MODE == P1_REAL) {
     for (int r = tj; r < L; r += TPC) {
       const uint32_t n = r * a.L2L3 + col_base + c;
@@ -175,6 +189,14 @@ __global__ void __launch_bounds__(kNcol * tpc_for<L>()) pass1_kernel(Pass1Args a
   if (MODE == P1_RESAMPLE || MODE == P1_CHIRP2 || MODE == P1_CHIRP1) {
     const double tot = block_sum<NT>(sum, red);
     if (threadIdx.x == 0) a.partials[static_cast<size_t>(b) * gridDim.x + blockIdx.x] = tot;
+  } else if (MODE == P1_CHIRP1_PAIR) {  // partial sums per template (2b, 2b + 1)
+    const double tot = block_sum<NT>(sum, red);
+    const double tot_b = block_sum<NT>(sum_b, red);
+    if (threadIdx.x == 0) {
+      a.partials[static_cast<size_t>(2 * b) * gridDim.x + blockIdx.x] = tot;
+      if (static_cast<uint32_t>(2 * b + 1) < a.n_tmpl)
+        a.partials[static_cast<size_t>(2 * b + 1) * gridDim.x + blockIdx.x] = tot_b;
+    }
   }
 }
 
@@ -328,6 +350,26 @@ pass1_pruned3_kernel(Pass1Args a) {
 }
 
 // ------------------------------------------------------------------ pass 2
+// mean-padding correction of the templates of transform b (one, or two for
+// paired chirp-z transforms), each reduced once in a fixed order:
+// delta[t] = (sum of pass 1's partial sums of template t) / n_steps
+template <int NT>
+__device__ __forceinline__ void reduce_delta(const Pass2Args& a, uint32_t b, double* red) {
+  const uint32_t tpt = a.tpt > 1 ? a.tpt : 1;
+  for (uint32_t q = 0; q < tpt; ++q) {
+    const uint32_t t = b * tpt + q;
+    if (tpt > 1 && t >= a.n_tmpl) break;  // uniform
+    const double* pp = a.partials + static_cast<size_t>(t) * a.n_partials;
+    double part = 0.0;
+    for (uint32_t i = threadIdx.x; i < a.n_partials; i += NT) part += pp[i];
+    const double tot = block_sum<NT>(part, red);
+    if (threadIdx.x == 0) {
+      const uint32_t n_s = a.tmpl[t].n_steps;
+      a.delta[t] = n_s ? tot / static_cast<double>(n_s) : 0.0;
+    }
+  }
+}
+
 // at least kMinWaves waves per SIMD: keeps the unrolled prefetch + FFT code
 // within 256 VGPRs (no spills) at 2 waves/SIMD
 constexpr int kMinWaves = 2;
@@ -402,17 +444,7 @@ __global__ void __launch_bounds__(kNcol * tpc_for<L>(), kMinWaves) pass2_kernel(
       v = cmul(v, cmul(wc, cmul(hi[e >> kP2LoBits], lo[e & (kLo - 1)])));
       base[static_cast<size_t>(k2) * a.L3 + c] = v;
     }
-    if (a.partials != nullptr && rem == 0) {
-      // mean-padding correction of template b, reduced once in a fixed order
-      const double* pp = a.partials + static_cast<size_t>(b) * a.n_partials;
-      double part = 0.0;
-      for (uint32_t i = threadIdx.x; i < a.n_partials; i += NT) part += pp[i];
-      const double tot = block_sum<NT>(part, red);
-      if (threadIdx.x == 0) {
-        const uint32_t n_s = a.tmpl[b].n_steps;
-        a.delta[b] = n_s ? tot / static_cast<double>(n_s) : 0.0;
-      }
-    }
+    if (a.partials != nullptr && rem == 0) reduce_delta<NT>(a, b, red);
     __syncthreads();  // LDS tile free for the next iteration
     tile = next;
   }
@@ -520,17 +552,7 @@ __global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_
       t0 = cmul(t0, step);
       t8 = cmul(t8, step);
     }
-    if (a.partials != nullptr && rem == 0) {
-      // mean-padding correction of template b, reduced once in a fixed order
-      const double* pp = a.partials + static_cast<size_t>(b) * a.n_partials;
-      double part = 0.0;
-      for (uint32_t i = threadIdx.x; i < a.n_partials; i += NT) part += pp[i];
-      const double tot = block_sum<NT>(part, red);
-      if (threadIdx.x == 0) {
-        const uint32_t n_s = a.tmpl[b].n_steps;
-        a.delta[b] = n_s ? tot / static_cast<double>(n_s) : 0.0;
-      }
-    }
+    if (a.partials != nullptr && rem == 0) reduce_delta<NT>(a, b, red);
     tile = next;
   }
 }
@@ -902,6 +924,7 @@ hipError_t launch_pass1(const FFTPlan3& plan, Pass1Mode mode, const Pass1Args& a
     else if (mode == P1_COMPLEX) hipLaunchKernelGGL((pass1_kernel<n, P1_COMPLEX>), grid, block, 0, s, a); \
     else if (mode == P1_CHIRP2) hipLaunchKernelGGL((pass1_kernel<n, P1_CHIRP2>), grid, block, 0, s, a);   \
     else if (mode == P1_CHIRP1) hipLaunchKernelGGL((pass1_kernel<n, P1_CHIRP1>), grid, block, 0, s, a);   \
+    else if (mode == P1_CHIRP1_PAIR) hipLaunchKernelGGL((pass1_kernel<n, P1_CHIRP1_PAIR>), grid, block, 0, s, a); \
     else hipLaunchKernelGGL((pass1_kernel<n, P1_COMPLEX_CONJ>), grid, block, 0, s, a);                 \
     break;                                                                                            \
   }

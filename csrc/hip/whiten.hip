@@ -263,6 +263,25 @@ __global__ void __launch_bounds__(NT) running_median_kernel(const float* in, uin
   }
 }
 
+// one output sample per thread; samples beyond the payload (odd n, 4-bit) are 0
+__global__ void unpack_kernel(const uint8_t* packed, uint32_t n_packed, bool four_bit, double scale, float* out,
+                              uint32_t n_out) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (i >= n_out) return;
+  float v = 0.0f;
+  if (four_bit) {
+    const uint32_t b = i >> 1;
+    if (b < n_packed) {
+      const uint8_t c = packed[b];
+      const uint32_t nib = (i & 1u) ? (c & 15u) : (c >> 4);
+      v = static_cast<float>(static_cast<double>(static_cast<float>(nib)) / scale);
+    }
+  } else if (i < n_packed) {
+    v = static_cast<float>(static_cast<double>(static_cast<int8_t>(packed[i])) / scale);
+  }
+  out[i] = v;
+}
+
 // spec[w2 + i] *= sqrt(ln2 / med[i]) for i < white_size
 __global__ void whiten_scale_kernel(float2* spec, const float* med, uint32_t white_size, uint32_t w2) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -302,6 +321,14 @@ __global__ void tangle_kernel(const float2* spec, uint32_t M, uint32_t fft_size,
 }
 
 }  // namespace
+
+hipError_t launch_unpack(const uint8_t* packed, uint32_t n_packed, bool four_bit, double scale, float* out,
+                         uint32_t n_out, hipStream_t s) {
+  if (n_out == 0) return hipSuccess;
+  hipLaunchKernelGGL(unpack_kernel, dim3((n_out + 255) / 256), dim3(256), 0, s, packed, n_packed, four_bit, scale, out,
+                     n_out);
+  return hipGetLastError();
+}
 
 hipError_t launch_whiten_power(const float2* spec, uint32_t n, float* ps, hipStream_t s) {
   hipLaunchKernelGGL(whiten_power_kernel, dim3((n + 255) / 256), dim3(256), 0, s, spec, n, ps);

@@ -11,6 +11,10 @@ namespace brp {
 namespace hipk {
 
 hipError_t launch_whiten_power(const float2* spec, uint32_t n, float* ps, hipStream_t s);
+// WU payload -> floats exactly as the host reader (demod_binary.c:830-842,
+// io.cpp): 4-bit high nibble first, (float)((double)v / scale); 8-bit signed
+hipError_t launch_unpack(const uint8_t* packed, uint32_t n_packed, bool four_bit, double scale, float* out,
+                         uint32_t n_out, hipStream_t s);
 bool running_median_supported(uint32_t W);
 hipError_t launch_running_median(const float* in, uint32_t n_in, uint32_t W, float* med, hipStream_t s);
 // any window (used above running_median_supported's limit): global radix sort

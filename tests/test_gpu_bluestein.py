@@ -137,19 +137,45 @@ def test_power_spectrum_bench_size(brp, gpu, padding, monkeypatch):
         assert err.max() < 2e-4, (N, padding, err.max(), int(np.argmax(err)) + 1)
 
 
-def test_bench_wu_p27_prefix_vs_cpu_golden(brp, gpu):
-    """The shipped WU at -P 2.7 -W (chirp-z path at bench size), first 50
-    templates, against the CPU golden model (tools/make_golden.py --end 50
-    --padding 2.7)."""
+@pytest.mark.parametrize("fA,end,golden", [(0.08, 50, "bench_wu_cpu_table_first50_P2.7.bin"),
+                                            (0.9999, 24, "bench_wu_cpu_table_first24_A0.9999_P2.7.bin")])
+def test_bench_wu_p27_prefix_vs_cpu_golden(brp, gpu, fA, end, golden):
+    """The shipped WU at -P 2.7 -W (chirp-z path at bench size, odd N: two
+    templates per transform), first templates against the CPU golden model
+    (tools/make_golden.py --end 50 --padding 2.7; --end 24 --fA 0.9999 for a
+    table with candidates on every level)."""
     from conftest import BANK, ROOT, WU, ZAP
     from test_gpu_search import _compare_tables
 
     cfg = SearchConfig.benchmark(str(WU), str(BANK), str(ZAP), batch=1)
     cfg.padding = 2.7
-    g = BRPSearch(cfg, pipelines=3).run(begin=0, end=50, write_output=False, use_checkpoint=False)
-    assert g.templates_run == 50 and g.geometry["nsamples"] == 11324621
+    cfg.fA = fA
+    g = BRPSearch(cfg, pipelines=3).run(begin=0, end=end, write_output=False, use_checkpoint=False)
+    assert g.templates_run == end and g.geometry["nsamples"] == 11324621
     gold = brp.CandidateTable()
-    gold.from_bytes(np.frombuffer((ROOT / "data" / "golden" / "bench_wu_cpu_table_first50_P2.7.bin").read_bytes(),
-                                  dtype=np.uint8).copy())
-    assert sum(1 for e in gold.entries() if e[5] > 0) > 20
+    gold.from_bytes(np.frombuffer((ROOT / "data" / "golden" / golden).read_bytes(), dtype=np.uint8).copy())
+    assert sum(1 for e in gold.entries() if e[5] > 0) >= (1 if fA < 0.5 else 40)
     _compare_tables(g.table, gold)
+
+
+def test_odd_length_template_pairs_match_single(brp, gpu, tmp_path, monkeypatch):
+    """Odd N runs two templates per chirp-z transform (x_a + i x_b, separated
+    by conjugate symmetry; P1_CHIRP1_PAIR): the candidate table matches the
+    one-template-per-transform path (BRP_BS_PAIR=0) and the CPU golden model,
+    with an odd number of templates per launch group (13 templates, groups of 2
+    and 3)."""
+    from test_gpu_search import _compare_tables
+
+    inj = synth.Injection(f0=211.0, P_orb=900.0, tau=0.03, psi0=0.7, amplitude=3.0)
+    case = synth.synthetic_case(tmp_path / "c", n=1 << 16, n_templates=12, inj=inj)
+    for batch in (2, 3):
+        cfg = dict(inputfile=case["wu"], templatebank=case["bank"], zaplistfile=case["zap"], f0=400.0,
+                   padding=2.3, fA=0.08, window=100, white=True, batch=batch)
+        pair = BRPSearch(SearchConfig(**cfg)).run(write_output=False, use_checkpoint=False)
+        monkeypatch.setenv("BRP_BS_PAIR", "0")
+        single = BRPSearch(SearchConfig(**cfg)).run(write_output=False, use_checkpoint=False)
+        monkeypatch.delenv("BRP_BS_PAIR")
+        assert pair.geometry["nsamples"] % 2 == 1
+        _compare_tables(pair.table, single.table, rtol=1e-5)
+        c = BRPSearch(SearchConfig(use_cpu=True, **cfg), gpus=8).run(write_output=False, use_checkpoint=False)
+        _compare_tables(pair.table, c.table)

@@ -57,10 +57,11 @@ def test_bounded_output_equals_compacting_path(brp, gpu, case, tmp_path, monkeyp
 
 
 def test_small_list_overflow_reruns_exactly(brp, gpu, case, tmp_path, monkeypatch):
-    """Fault injection: a 64-slot list (BRP_HS_CAP) overflows in the early
-    batches (empty table, chi^2 thresholds only); those batches are re-run
-    with the bounded output and the table is the default run's, byte for byte.
-    Three pipelines, two batches in flight each."""
+    """Fault injection: a small list (BRP_HS_CAP; the engine keeps it at the
+    bounded output's size, 8 templates x 5 levels x 128 slots) overflows on the
+    raw series' batches; those batches are re-run with the bounded output and
+    the table is the default run's, byte for byte. Three pipelines, two
+    batches in flight each."""
     ref = _run(_cfg(case, tmp_path / "a", white=False, batch=2), pipelines=3)
     monkeypatch.setenv("BRP_HS_CAP", "64")
     small = _run(_cfg(case, tmp_path / "b", white=False, batch=2), pipelines=3)

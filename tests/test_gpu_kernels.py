@@ -328,3 +328,23 @@ def test_running_median_kernel_bit_exact(brp, gpu, w):
     got, _ = brp.hip_running_median(x, w)
     assert got.shape == ref.shape
     assert np.array_equal(got, ref)
+
+
+@pytest.mark.parametrize("four_bit", [True, False])
+def test_device_unpack_bit_exact(brp, gpu, tmp_path, four_bit):
+    """The device unpacks the WU payload (HipEngine.setup_packed: n/2 bytes over
+    PCIe instead of 4n) to exactly the floats of the host reader
+    (io.cpp, demod_binary.c:830-842): 4-bit high nibble first, 8-bit signed,
+    value / scale in double. Odd sample count included."""
+    from boinc_app_eah_brp_amd.utils import synth
+
+    x = synth.make_series((1 << 14) + 1, 65.476, None)
+    wu = synth.write_wu(tmp_path / ("a.bin4" if four_bit else "a.binary"), x, four_bit=four_bit, scale=0.37)
+    hdr, series, _ = brp.read_work_unit(str(wu))
+    geom = brp.derive_geometry(hdr, dict(f0=150.0, padding=2.0, fA=0.08, window=100))
+    eng = brp.HipEngine()
+    eng.init(0, 1)
+    eng.setup_from_wu(geom, str(wu), 0.0)
+    dev = eng.download_series()
+    assert dev.dtype == np.float32 and dev.size == series.size
+    assert np.array_equal(dev.view(np.uint32), np.asarray(series, np.float32).view(np.uint32))
