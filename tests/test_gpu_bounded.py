@@ -58,13 +58,14 @@ def test_bounded_output_equals_compacting_path(brp, gpu, case, tmp_path, monkeyp
 
 def test_small_list_overflow_reruns_exactly(brp, gpu, case, tmp_path, monkeypatch):
     """Fault injection: a small list (BRP_HS_CAP; the engine keeps it at the
-    bounded output's size, 8 templates x 5 levels x 128 slots) overflows on the
-    raw series' batches; those batches are re-run with the bounded output and
-    the table is the default run's, byte for byte. Three pipelines, two
-    batches in flight each."""
-    ref = _run(_cfg(case, tmp_path / "a", white=False, batch=2), pipelines=3)
+    bounded output's size, 8 templates x 5 levels x 128 slots) overflows at
+    -A 1; those batches are re-run with the bounded output and the table is
+    the default run's (whose 2^20-slot lists hold everything), byte for byte.
+    Three pipelines, two batches in flight each."""
+    # -A 1: zero thresholds, every bin of [w2, fhi) is above them (~25 k values per template)
+    ref = _run(_cfg(case, tmp_path / "a", fA=1.0, batch=2), pipelines=3)
     monkeypatch.setenv("BRP_HS_CAP", "64")
-    small = _run(_cfg(case, tmp_path / "b", white=False, batch=2), pipelines=3)
+    small = _run(_cfg(case, tmp_path / "b", fA=1.0, batch=2), pipelines=3)
     assert small.stats["overflow_reruns"] > 0, small.stats
     assert bytes(small.table.to_bytes()) == bytes(ref.table.to_bytes())
 
