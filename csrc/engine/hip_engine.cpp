@@ -252,6 +252,7 @@ std::vector<float2> stage_table_rows(uint32_t L) {
 // so they are computed once: ~80 000 long-double sin/cos per plan.
 struct HostTables {
   std::vector<float2> st1, st2, st3, p1, p2col, p2lo, p2hi, p3;
+  std::vector<float2> a512, a48;  // two-pass plan: W_512^e, W_48^e
 };
 
 const HostTables& host_tables(const FFTPlan3& plan) {
@@ -281,6 +282,10 @@ const HostTables& host_tables(const FFTPlan3& plan) {
   h->p3.assign(32 + 4ull * L3 / 32, make_float2(0, 0));
   for (uint32_t i = 0; i < 32; ++i) h->p3[i] = root(i, 4ull * L3);
   for (uint32_t m = 0; m < 4 * L3 / 32; ++m) h->p3[32 + m] = root(32ull * m, 4ull * L3);
+  h->a512.resize(512);
+  for (uint32_t e = 0; e < 512; ++e) h->a512[e] = root(e, 512);
+  h->a48.resize(48);
+  for (uint32_t e = 0; e < 48; ++e) h->a48[e] = root(e, 48);
   slot = std::move(h);
   return *slot;
 }
@@ -480,6 +485,12 @@ struct HipEngine::Impl {
     w_pending = false;
   }
   DevBuf<float2> t_st1, t_st2, t_st3, t_p1, t_p2col, t_p2lo, t_p2hi, t_p3;
+  DevBuf<float2> t_a512, t_a48;
+  // Two-pass plan for the benchmark geometry (fft_two_pass.hip): pass A = the
+  // resampling gather and the whole 24576-point column transform, pass B =
+  // pass 3 on transposed row tiles; 100 MB less memory traffic per template
+  // than the three passes. Opt-in (BRP_TWO_PASS=1) while it is slower.
+  bool two_pass = false;
 
   struct { TemplateDev* p = nullptr; } h_tmpl;
   struct { float* p = nullptr; } h_thr;
@@ -517,7 +528,8 @@ struct HipEngine::Impl {
     int rc;
     if ((rc = upload(t_st1, h.st1)) || (rc = upload(t_st2, h.st2)) || (rc = upload(t_st3, h.st3)) ||
         (rc = upload(t_p1, h.p1)) || (rc = upload(t_p2col, h.p2col)) || (rc = upload(t_p2lo, h.p2lo)) ||
-        (rc = upload(t_p2hi, h.p2hi)) || (rc = upload(t_p3, h.p3)))
+        (rc = upload(t_p2hi, h.p2hi)) || (rc = upload(t_p3, h.p3)) || (rc = upload(t_a512, h.a512)) ||
+        (rc = upload(t_a48, h.a48)))
       return rc;
     return 0;
   }
@@ -676,48 +688,92 @@ struct HipEngine::Impl {
     if (stream) (void)hipStreamDestroy(stream);
   }
 
+  // Template transform up to the complex array: pass 1 (+ pass 2), or pass A
+  // of the two-pass plan. `reset`: the batch's candidate counter to zero.
+  hipError_t fft_pass1(int nb, uint32_t* reset) {
+    const hipk::TwiddleTable tw = twt();
+    if (two_pass) {
+      hipk::PassAArgs aa{};
+      aa.out = buf.p;
+      aa.tw = tw;
+      aa.w512 = t_a512.p;
+      aa.w48 = t_a48.p;
+      aa.series = series_in();
+      aa.n_unpadded = g.n_unpadded;
+      aa.tmpl = tmpl.p;
+      aa.partials = partials.p;
+      aa.reset = reset;
+      return hipk::launch_pass_a(plan, aa, nb, stream);
+    }
+    hipk::Pass1Args a1{};
+    a1.out = buf.p;
+    a1.L2L3 = plan.L2 * plan.L3;
+    a1.L3 = plan.L3;
+    a1.tw = tw;
+    a1.tb = tables();
+    a1.series = series_in();
+    a1.n_unpadded = g.n_unpadded;
+    a1.tmpl = tmpl.p;
+    a1.partials = partials.p;
+    a1.reset = reset;
+    return hipk::launch_pass1(plan, hipk::P1_RESAMPLE, a1, nb, stream);
+  }
+  hipError_t fft_pass2(int nb) {
+    if (two_pass) return hipSuccess;  // pass A did the whole column transform
+    hipk::Pass2Args a2{};
+    a2.buf = buf.p;
+    a2.L1 = plan.L1;
+    a2.L2L3 = plan.L2 * plan.L3;
+    a2.L3 = plan.L3;
+    a2.tw = twt();
+    a2.tb = tables();
+    a2.partials = partials.p;
+    a2.n_partials = plan.wg1();
+    a2.tmpl = tmpl.p;
+    a2.delta = delta.p;
+    return hipk::launch_pass2(plan, a2, nb, stream);
+  }
+  // row pass + untangle + power spectrum into out[b * stride + k], k < limit
+  hipError_t fft_pass3(int nb, float* out, _Float16* out16, uint32_t stride, uint32_t limit) {
+    hipk::Pass3Args a3{};
+    a3.buf = buf.p;
+    a3.L1 = plan.L1;
+    a3.L2 = plan.L2;
+    a3.L3 = plan.L3;
+    a3.C = plan.L1 * plan.L2;
+    a3.M = plan.M;
+    a3.tw = twt();
+    a3.tb = tables();
+    a3.limit = limit;
+    a3.ps = out;
+    a3.ps16 = out16;
+    a3.ps_stride = stride;
+    a3.norm = static_cast<float>(1.0 / g.nsamples);
+    a3.tmpl = tmpl.p;
+    a3.delta = delta.p;
+    a3.tp = two_pass;
+    a3.partials = partials.p;
+    a3.n_partials = plan.L3;  // pass A: one partial sum per column n3
+    return hipk::launch_pass3(plan, hipk::P3_POWER, a3, nb, stream);
+  }
+
   // Pipeline stages of one batch; the whole sequence is captured into a graph.
   enum Stage { kPrologue = 0, kPass1, kPass2, kPass3, kHarmonic, kEpilogue, kNumStages };
 
   hipError_t enqueue_stage(int st, int nb) {
     hipError_t e = hipSuccess;
-    const hipk::TwiddleTable tw = twt();
     switch (st) {
       case kPrologue:
         // n_steps comes with the parameters (host bracketed search); pass 1
         // zeroes the batch's candidate counter
         if (fg_in) return hipSuccess;  // the host wrote `in` directly
         return hipMemcpyAsync(in.p, h_in.p, thr_bytes + sizeof(TemplateDev) * nb, hipMemcpyHostToDevice, stream);
-      case kPass1: {
+      case kPass1:
         if (bs) return bs_template_in(nb, group_reset ? &cands.p[0].x : nullptr);
-        hipk::Pass1Args a1{};
-        a1.out = buf.p;
-        a1.L2L3 = plan.L2 * plan.L3;
-        a1.L3 = plan.L3;
-        a1.tw = tw;
-        a1.tb = tables();
-        a1.series = series_in();
-        a1.n_unpadded = g.n_unpadded;
-        a1.tmpl = tmpl.p;
-        a1.partials = partials.p;
-        a1.reset = group_reset ? &cands.p[0].x : nullptr;
-        return hipk::launch_pass1(plan, hipk::P1_RESAMPLE, a1, nb, stream);
-      }
-      case kPass2: {
+        return fft_pass1(nb, group_reset ? &cands.p[0].x : nullptr);
+      case kPass2:
         if (bs) return bs_template_round0(nb);
-        hipk::Pass2Args a2{};
-        a2.buf = buf.p;
-        a2.L1 = plan.L1;
-        a2.L2L3 = plan.L2 * plan.L3;
-        a2.L3 = plan.L3;
-        a2.tw = tw;
-        a2.tb = tables();
-        a2.partials = partials.p;
-        a2.n_partials = plan.wg1();
-        a2.tmpl = tmpl.p;
-        a2.delta = delta.p;
-        return hipk::launch_pass2(plan, a2, nb, stream);
-      }
+        return fft_pass2(nb);
       case kPass3: {
         if (bs) {
           const hipError_t e3 = bs_round(bs_trans(nb), 1);
@@ -725,23 +781,8 @@ struct HipEngine::Impl {
           return bs_template_power(nb, ps.p, ps_fp16 ? reinterpret_cast<_Float16*>(ps.p) : nullptr, ps_stride,
                                    std::min(g.harmonic_idx_hi, g.fft_size));
         }
-        hipk::Pass3Args a3{};
-        a3.buf = buf.p;
-        a3.L1 = plan.L1;
-        a3.L2 = plan.L2;
-        a3.L3 = plan.L3;
-        a3.C = plan.L1 * plan.L2;
-        a3.M = plan.M;
-        a3.tw = tw;
-        a3.tb = tables();
-        a3.limit = std::min(g.harmonic_idx_hi, g.fft_size);
-        a3.ps = ps.p;
-        a3.ps16 = ps_fp16 ? reinterpret_cast<_Float16*>(ps.p) : nullptr;
-        a3.ps_stride = ps_stride;
-        a3.norm = static_cast<float>(1.0 / g.nsamples);
-        a3.tmpl = tmpl.p;
-        a3.delta = delta.p;
-        return hipk::launch_pass3(plan, hipk::P3_POWER, a3, nb, stream);
+        return fft_pass3(nb, ps.p, ps_fp16 ? reinterpret_cast<_Float16*>(ps.p) : nullptr, ps_stride,
+                         std::min(g.harmonic_idx_hi, g.fft_size));
       }
       case kHarmonic: {
         hipk::HSArgs ah{};
@@ -1066,6 +1107,8 @@ int HipEngine::setup_impl(const SearchGeometry& g, const float* host_series, con
   if (wis.persist_per_cu >= 0) d.persist_per_cu = static_cast<uint32_t>(wis.persist_per_cu);
   if (const char* e = std::getenv("BRP_PERSIST")) d.persist_per_cu = static_cast<uint32_t>(std::atoi(e));
   d.plan.persist_wgs = d.persist_per_cu * d.num_cus;
+  d.two_pass = !d.bs && hipk::two_pass_supported(d.plan, g.n_unpadded) && std::getenv("BRP_TWO_PASS") != nullptr &&
+               std::atoi(std::getenv("BRP_TWO_PASS")) != 0;
   log_message(LOG_DEBUG, true, "FFT plan: N=%u M=%u = %u x %u x %u\n", g.nsamples, d.plan.M, d.plan.L1, d.plan.L2,
               d.plan.L3);
   const uint32_t limit = std::min(g.harmonic_idx_hi, g.fft_size);
@@ -1652,7 +1695,6 @@ int HipEngine::power_spectrum(const TemplateInput& t, std::vector<float>& ps_out
     BRP_HIP_CHECK(hipMemcpyAsync(d.tmpl.p, d.h_tmpl.p, sizeof(TemplateDev), hipMemcpyHostToDevice, s),
                   RADPUL_HIP_MEM_COPY_HOST_DEVICE);
   std::atomic_thread_fence(std::memory_order_seq_cst);
-  const hipk::TwiddleTable tw = d.twt();
   if (d.bs) {
     DevBuf<float> full;
     int rc;
@@ -1665,48 +1707,12 @@ int HipEngine::power_spectrum(const TemplateInput& t, std::vector<float>& ps_out
     if (n_steps) *n_steps = d.h_tmpl.p[0].n_steps;
     return 0;
   }
-  hipk::Pass1Args a1{};
-  a1.out = d.buf.p;
-  a1.L2L3 = d.plan.L2 * d.plan.L3;
-  a1.L3 = d.plan.L3;
-  a1.tw = tw;
-  a1.tb = d.tables();
-  a1.series = d.series_in();
-  a1.n_unpadded = g.n_unpadded;
-  a1.tmpl = d.tmpl.p;
-  a1.partials = d.partials.p;
-  BRP_HIP_CHECK(hipk::launch_pass1(d.plan, hipk::P1_RESAMPLE, a1, 1, s), RADPUL_HIP_KERNEL_INVOKE);
-  hipk::Pass2Args a2{};
-  a2.buf = d.buf.p;
-  a2.L1 = d.plan.L1;
-  a2.L2L3 = d.plan.L2 * d.plan.L3;
-  a2.L3 = d.plan.L3;
-  a2.tw = tw;
-  a2.tb = d.tables();
-  a2.partials = d.partials.p;
-  a2.n_partials = d.plan.wg1();
-  a2.tmpl = d.tmpl.p;
-  a2.delta = d.delta.p;
-  BRP_HIP_CHECK(hipk::launch_pass2(d.plan, a2, 1, s), RADPUL_HIP_KERNEL_INVOKE);
+  BRP_HIP_CHECK(d.fft_pass1(1, nullptr), RADPUL_HIP_KERNEL_INVOKE);
+  BRP_HIP_CHECK(d.fft_pass2(1), RADPUL_HIP_KERNEL_INVOKE);
   DevBuf<float> full;
   int rc;
   if ((rc = full.alloc(g.fft_size))) return rc;
-  hipk::Pass3Args a3{};
-  a3.buf = d.buf.p;
-  a3.L1 = d.plan.L1;
-  a3.L2 = d.plan.L2;
-  a3.L3 = d.plan.L3;
-  a3.C = d.plan.L1 * d.plan.L2;
-  a3.M = d.plan.M;
-  a3.tw = tw;
-  a3.tb = d.tables();
-  a3.limit = g.fft_size;
-  a3.ps = full.p;
-  a3.ps_stride = g.fft_size;
-  a3.norm = static_cast<float>(1.0 / g.nsamples);
-  a3.tmpl = d.tmpl.p;
-  a3.delta = d.delta.p;
-  BRP_HIP_CHECK(hipk::launch_pass3(d.plan, hipk::P3_POWER, a3, 1, s), RADPUL_HIP_KERNEL_INVOKE);
+  BRP_HIP_CHECK(d.fft_pass3(1, full.p, nullptr, g.fft_size, g.fft_size), RADPUL_HIP_KERNEL_INVOKE);
   ps_out.resize(g.fft_size);
   BRP_HIP_CHECK(hipMemcpyAsync(ps_out.data(), full.p, g.fft_size * sizeof(float), hipMemcpyDeviceToHost, s),
                 RADPUL_HIP_MEM_COPY_DEVICE_HOST);

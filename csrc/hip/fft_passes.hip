@@ -638,13 +638,17 @@ struct P3Emit {
   }
 };
 
-template <int L, int ROWS, int MODE>
+// TP: pass B of the two-pass plan (fft_two_pass.hip). The rows come from pass
+// A's transposed output ([n3][tp_pos(c)]: lanes walk the workgroup's rows, so
+// the loads are row-block pieces) into a column-interleaved LDS block, which
+// keeps those LDS writes conflict-free; delta is reduced from pass A's sums.
+template <int L, int ROWS, int MODE, bool TP = false>
 __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Args a) {
   constexpr int TPC = tpc_for<L>();
   constexpr int NSLOT = 2 * ROWS;
   constexpr int NT = NSLOT * TPC;
   constexpr int L4 = 4 * L;
-  using Lay = BlockLayout<L, NSLOT, TPC, true>;
+  using Lay = BlockLayout<L, NSLOT, TPC, !TP>;
   // data | stage twiddles W_L | W_{4L} (= W_2N^{C i}) as lo[32] | hi[4L/32]
   constexpr int kT4 = 32 + L4 / 32;
   static_assert(L4 % 32 == 0, "two-level W_{4L} table");
@@ -665,7 +669,7 @@ __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Arg
   // j = tj + TPC u reads elements j + (L/R0) q of its row (lanes walk j:
   // contiguous 8-B loads), transforms in registers and writes its Stockham
   // output rows R0 j + q to LDS; the remaining stages run LDS -> LDS
-  constexpr int R0 = BlockFFT<L, NSLOT, TPC, true>::kFirstRadix;
+  constexpr int R0 = BlockFFT<L, NSLOT, TPC, !TP>::kFirstRadix;
   constexpr int kBf0 = L / R0;
   // Measured on MI355X (L = 256): 16-B row loads into LDS beat the 8-B loads
   // the register first stage needs (18.2 vs 18.9 us/template), so the
@@ -692,7 +696,26 @@ __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Arg
     }
     if (threadIdx.x < kT4) t4v = a.tb.p3[threadIdx.x];
   };
-  if constexpr (!kRegStage1) {
+  if constexpr (TP) {
+    // element f = tid + NT u: row slot f % NSLOT, column n3 = f / NSLOT
+    constexpr int kPer = L * NSLOT / NT;
+    static_assert((L * NSLOT) % NT == 0, "whole tile-load iterations");
+    float2 rv[kPer];
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int f = static_cast<int>(threadIdx.x) + u * NT;
+      const int slot = f % NSLOT, n3 = f / NSLOT;
+      const uint32_t cs = c0 + (slot % ROWS);
+      const uint32_t row = (slot < ROWS) ? cs : (a.C - cs) % a.C;
+      rv[u] = buf[static_cast<size_t>(n3) * a.C + tp_pos(row < a.C ? row : 0)];
+    }
+    load_tables();
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int f = static_cast<int>(threadIdx.x) + u * NT;
+      data[Lay::idx(f / NSLOT, f % NSLOT)] = rv[u];
+    }
+  } else if constexpr (!kRegStage1) {
     int slot, tj;
     Lay::coords(threadIdx.x, slot, tj);
     const uint32_t cs = c0 + (slot % ROWS);
@@ -741,7 +764,16 @@ __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Arg
   uint32_t n_s = 0;
   if (MODE == P3_POWER || MODE == P3_POWER16) {
     n_s = a.tmpl[b].n_steps;
-    delta = a.delta[b];
+    if constexpr (!TP) delta = a.delta[b];
+  }
+  if constexpr (TP) {
+    // pass A's per-column sums, reduced in a fixed order by every workgroup
+    __shared__ double red[NT / kWave + 1];
+    double part = 0.0;
+    const double* pp = a.partials + static_cast<size_t>(b) * a.n_partials;
+    for (uint32_t i = threadIdx.x; i < a.n_partials; i += NT) part += pp[i];
+    const double tot = block_sum<NT>(part, red);
+    delta = n_s ? tot / static_cast<double>(n_s) : 0.0;
   }
   // per-row twiddle constants of the untangle phase, fetched before the FFT so
   // their latency hides under it
@@ -752,8 +784,8 @@ __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Arg
   const uint32_t half = a.C / 2;
   const RowTw rt = row_twiddles(a.tw, c, n_s);
   __syncthreads();
-  if constexpr (kRegStage1) BlockFFT<L, NSLOT, TPC, true>::run_rest(data, twl);
-  else if constexpr (!kAblateP3Fft) BlockFFT<L, NSLOT, TPC, true>::run(data, twl);
+  if constexpr (kRegStage1 && !TP) BlockFFT<L, NSLOT, TPC, true>::run_rest(data, twl);
+  else if constexpr (!kAblateP3Fft) BlockFFT<L, NSLOT, TPC, !TP>::run(data, twl);
 
   constexpr bool kPower = (MODE == P3_POWER || MODE == P3_POWER16);
   const bool correct = kPower && n_s > 0;
@@ -963,7 +995,20 @@ hipError_t launch_pass2(const FFTPlan3& plan, const Pass2Args& a, int batch, hip
 
 constexpr int kRows3 = 8;
 
+#ifndef BRP_TP_ROWS
+#define BRP_TP_ROWS 24  // pass B rows per workgroup (one 24-row block of pass A's layout)
+#endif
+constexpr int kRowsTp = BRP_TP_ROWS;
+
 hipError_t launch_pass3(const FFTPlan3& plan, Pass3Mode mode, const Pass3Args& a, int batch, hipStream_t s) {
+  if (a.tp) {
+    if (plan.L3 != 256 || a.C % 24 != 0 || mode == P3_COMPLEX) return hipErrorInvalidValue;
+    const dim3 grid((a.C / 2 + kRowsTp) / kRowsTp, batch);
+    const dim3 block(2 * kRowsTp * tpc_for<256>());
+    if (a.ps16) hipLaunchKernelGGL((pass3_kernel<256, kRowsTp, P3_POWER16, true>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((pass3_kernel<256, kRowsTp, P3_POWER, true>), grid, block, 0, s, a);
+    return hipGetLastError();
+  }
   if (plan.rows3 != kRows3) return hipErrorInvalidValue;
   const dim3 grid(plan.wg3(), batch);
   switch (plan.L3) {

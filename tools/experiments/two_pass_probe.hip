@@ -10,7 +10,8 @@
 //   A : gather 8192 complex (the non-padding third) at stride 256 complex,
 //       3 x 3 LDS round trips of 64 KB (the FFT's exchanges), write 24576
 //       complex contiguous                                   (17 + 50 MB)
-//   A0: A without the LDS round trips (gather + write only)
+//   A0: A without the LDS round trips (gather + write only); A_conflict_free_R:
+//       R round trips per set with lane-consecutive (conflict-free) addresses
 //   B : 16 rows + their 16 mirror rows per workgroup read as 2 x 256 pieces
 //       of 128 B, powers written as 64-B pieces of bins c + C k3 (50 + 21 MB)
 //   P1/P2/P3: today's passes as memory shapes (16-column gather + write;
@@ -42,7 +43,7 @@ __device__ __forceinline__ uint32_t xcd_col(uint32_t b, uint32_t n) {
   return (b % 8) * (n / 8) + b / 8;
 }
 
-template <bool LDS>
+template <bool LDS, int ROUNDS = 3, bool CONFLICT = true>
 __global__ void __launch_bounds__(1024) passA(const float* __restrict__ ser, float2* __restrict__ out) {
   __shared__ float2 lds[8192];
   const uint32_t n3 = xcd_col(blockIdx.x, L3);
@@ -60,14 +61,15 @@ __global__ void __launch_bounds__(1024) passA(const float* __restrict__ ser, flo
   if constexpr (LDS) {
     for (int s = 0; s < 3; ++s) {
 #pragma unroll
-      for (int r = 0; r < 3; ++r) {
+      for (int r = 0; r < ROUNDS; ++r) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) lds[t + 1024 * j] = v[8 * s + j];
         __syncthreads();
         // transposed read: butterfly-like stride
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float2 w = lds[((t * 8 + j) * (r + 1)) & 8191];
+          const float2 w = CONFLICT ? lds[((t * 8 + j) * (r + 1)) & 8191]
+                                    : lds[(t ^ (64 * (r + 1))) + 1024 * ((j + r) & 7)];  // lanes consecutive
           v[8 * s + j] = make_float2(v[8 * s + j].x + w.y, v[8 * s + j].y - w.x);
         }
         __syncthreads();
@@ -77,6 +79,48 @@ __global__ void __launch_bounds__(1024) passA(const float* __restrict__ ser, flo
   float2* o = out + (static_cast<size_t>(blockIdx.y) * L3 + n3) * C;
 #pragma unroll
   for (int j = 0; j < 24; ++j) o[t + 1024 * j] = v[j];
+}
+
+// A with 512 threads: the 16 gathered inputs stay in registers and each set
+// (output residue r) is formed, exchanged and stored in turn; two workgroups
+// per CU, so one workgroup's LDS phase overlaps the other's memory phase
+template <int ROUNDS, bool STRIDE3 = false>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) passA512(const float* __restrict__ ser, float2* __restrict__ out) {
+  __shared__ float2 lds[8192];
+  const uint32_t n3 = xcd_col(blockIdx.x, L3);
+  const uint32_t t = threadIdx.x;
+  float2 v[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const uint32_t np = t + 512 * j;
+    const uint32_t n = (np >> 7) * (L2 * L3) + (np & 127) * L3 + n3;
+    const uint32_t m = (2 * n + 17 * blockIdx.y) & (NSER - 2);
+    v[j] = make_float2(ser[m], ser[m + 1]);
+  }
+  float2* o = out + (static_cast<size_t>(blockIdx.y) * L3 + n3) * C;
+  for (int s = 0; s < 3; ++s) {
+    float2 w[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) w[j] = make_float2(v[j].x * (s + 1), v[j].y - s);
+#pragma unroll
+    for (int r = 0; r < ROUNDS; ++r) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) lds[t + 512 * j] = w[j];
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const float2 x = lds[(t ^ (64 * (r + 1))) + 512 * ((j + r) & 15)];
+        w[j] = make_float2(w[j].x + x.y, w[j].y - x.x);
+      }
+      __syncthreads();
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      // set-major [r][q], or natural order c = 3 q + r (stride-3 stores, the lines merge in L2)
+      const uint32_t q = t + 512 * j;
+      o[STRIDE3 ? 3 * q + s : 8192 * s + q] = w[j];
+    }
+  }
 }
 
 // 16 rows c0.. + mirror rows, 256 threads: thread (tile h, n3 quarter)
@@ -191,14 +235,19 @@ int main() {
     return 1e3f * ms / reps / T;  // per template
   };
   const float tA = timeit([&] { hipLaunchKernelGGL((passA<true>), dim3(L3, T), dim3(1024), 0, 0, ser, buf2); });
+  const float tAc3 = timeit([&] { hipLaunchKernelGGL((passA<true, 3, false>), dim3(L3, T), dim3(1024), 0, 0, ser, buf2); });
+  const float tAc2 = timeit([&] { hipLaunchKernelGGL((passA<true, 2, false>), dim3(L3, T), dim3(1024), 0, 0, ser, buf2); });
+  const float t5123 = timeit([&] { hipLaunchKernelGGL((passA512<3>), dim3(L3, T), dim3(512), 0, 0, ser, buf2); });
+  const float t5122 = timeit([&] { hipLaunchKernelGGL((passA512<2>), dim3(L3, T), dim3(512), 0, 0, ser, buf2); });
+  const float t512s = timeit([&] { hipLaunchKernelGGL((passA512<3, true>), dim3(L3, T), dim3(512), 0, 0, ser, buf2); });
   const float tA0 = timeit([&] { hipLaunchKernelGGL((passA<false>), dim3(L3, T), dim3(1024), 0, 0, ser, buf2); });
   const float tB = timeit([&] { hipLaunchKernelGGL(passB, dim3(C / 32, T), dim3(512), 0, 0, buf2, ps); });
   const float t1 = timeit([&] { hipLaunchKernelGGL(p1, dim3(L2 * 16, T), dim3(256), 0, 0, ser, buf); });
   const float t2 = timeit([&] { hipLaunchKernelGGL(p2, dim3(L1 * 16, T), dim3(128), 0, 0, buf); });
   const float t3 = timeit([&] { hipLaunchKernelGGL(p3, dim3(C / 16, T), dim3(512), 0, 0, buf, ps); });
   CHECK(hipDeviceSynchronize());
-  std::printf("{\"us_per_template\": {\"A_gather_lds_write\": %.2f, \"A0_gather_write\": %.2f, \"B_tiles_ps\": %.2f, "
+  std::printf("{\"us_per_template\": {\"A_gather_lds_write\": %.2f, \"A_conflict_free_3\": %.2f, \"A_conflict_free_2\": %.2f, \"A512_3\": %.2f, \"A512_2\": %.2f, \"A512_3_stride3\": %.2f, \"A0_gather_write\": %.2f, \"B_tiles_ps\": %.2f, "
               "\"two_pass_total\": %.2f, \"p1\": %.2f, \"p2\": %.2f, \"p3\": %.2f, \"three_pass_total\": %.2f}}\n",
-              tA, tA0, tB, tA + tB, t1, t2, t3, t1 + t2 + t3);
+              tA, tAc3, tAc2, t5123, t5122, t512s, tA0, tB, tA + tB, t1, t2, t3, t1 + t2 + t3);
   return 0;
 }
