@@ -252,7 +252,7 @@ std::vector<float2> stage_table_rows(uint32_t L) {
 // so they are computed once: ~80 000 long-double sin/cos per plan.
 struct HostTables {
   std::vector<float2> st1, st2, st3, p1, p2col, p2lo, p2hi, p3;
-  std::vector<float2> a512, a48;  // two-pass plan: W_512^e, W_48^e
+  std::vector<float2> a1024, a48;  // two-pass plan: W_1024^e, W_48^e
 };
 
 const HostTables& host_tables(const FFTPlan3& plan) {
@@ -282,8 +282,8 @@ const HostTables& host_tables(const FFTPlan3& plan) {
   h->p3.assign(32 + 4ull * L3 / 32, make_float2(0, 0));
   for (uint32_t i = 0; i < 32; ++i) h->p3[i] = root(i, 4ull * L3);
   for (uint32_t m = 0; m < 4 * L3 / 32; ++m) h->p3[32 + m] = root(32ull * m, 4ull * L3);
-  h->a512.resize(512);
-  for (uint32_t e = 0; e < 512; ++e) h->a512[e] = root(e, 512);
+  h->a1024.resize(1024);
+  for (uint32_t e = 0; e < 1024; ++e) h->a1024[e] = root(e, 1024);
   h->a48.resize(48);
   for (uint32_t e = 0; e < 48; ++e) h->a48[e] = root(e, 48);
   slot = std::move(h);
@@ -485,7 +485,7 @@ struct HipEngine::Impl {
     w_pending = false;
   }
   DevBuf<float2> t_st1, t_st2, t_st3, t_p1, t_p2col, t_p2lo, t_p2hi, t_p3;
-  DevBuf<float2> t_a512, t_a48;
+  DevBuf<float2> t_a1024, t_a48;
   // Two-pass plan for the benchmark geometry (fft_two_pass.hip): pass A = the
   // resampling gather and the whole 24576-point column transform, pass B =
   // pass 3 on transposed row tiles; 100 MB less memory traffic per template
@@ -528,7 +528,7 @@ struct HipEngine::Impl {
     int rc;
     if ((rc = upload(t_st1, h.st1)) || (rc = upload(t_st2, h.st2)) || (rc = upload(t_st3, h.st3)) ||
         (rc = upload(t_p1, h.p1)) || (rc = upload(t_p2col, h.p2col)) || (rc = upload(t_p2lo, h.p2lo)) ||
-        (rc = upload(t_p2hi, h.p2hi)) || (rc = upload(t_p3, h.p3)) || (rc = upload(t_a512, h.a512)) ||
+        (rc = upload(t_p2hi, h.p2hi)) || (rc = upload(t_p3, h.p3)) || (rc = upload(t_a1024, h.a1024)) ||
         (rc = upload(t_a48, h.a48)))
       return rc;
     return 0;
@@ -696,7 +696,7 @@ struct HipEngine::Impl {
       hipk::PassAArgs aa{};
       aa.out = buf.p;
       aa.tw = tw;
-      aa.w512 = t_a512.p;
+      aa.w1024 = t_a1024.p;
       aa.w48 = t_a48.p;
       aa.series = series_in();
       aa.n_unpadded = g.n_unpadded;

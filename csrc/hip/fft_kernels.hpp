@@ -140,7 +140,7 @@ struct Pass3PlainArgs {
 struct PassAArgs {
   float2* out;                 // [batch][L3][C]
   TwiddleTable tw;             // W_2N (N = fft size)
-  const float2* w512;          // W_512^e, e < 512
+  const float2* w1024;         // W_1024^e, e < 1024
   const float2* w48;           // W_48^e, e < 48
   const float* series;         // [slots][n_unpadded]
   uint32_t n_unpadded;
@@ -148,8 +148,18 @@ struct PassAArgs {
   double* partials;            // [batch][L3] sums of (sample - mu0)
   uint32_t* reset;             // zeroed by workgroup (0, 0) when non-null
 };
-// row position of row c within a column of pass A's output
-__host__ __device__ inline uint32_t tp_pos(uint32_t c) { return 24u * (c / 24u) + 8u * (c % 3u) + (c % 24u) / 3u; }
+// Row position of row c = 3 q + r within a column of pass A's output: blocks
+// of kTpBlock rows, inside a block set-major ([r][q % (kTpBlock / 3)]), so a
+// set's kTpBlock / 3 consecutive q are one contiguous piece of pass A's stores
+// and a block of rows is one contiguous piece of pass B's loads.
+#ifndef BRP_TP_BLOCK
+#define BRP_TP_BLOCK 24
+#endif
+constexpr uint32_t kTpBlock = BRP_TP_BLOCK;
+static_assert(kTpBlock % 3 == 0 && 512 % (kTpBlock / 3) == 0, "pass A layout block");
+__host__ __device__ inline uint32_t tp_pos(uint32_t c) {
+  return kTpBlock * (c / kTpBlock) + (kTpBlock / 3) * (c % 3u) + (c % kTpBlock) / 3u;
+}
 bool two_pass_supported(const FFTPlan3& plan, uint32_t n_unpadded);
 hipError_t launch_pass_a(const FFTPlan3& plan, const PassAArgs& a, int batch, hipStream_t s);
 

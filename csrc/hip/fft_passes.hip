@@ -996,13 +996,13 @@ hipError_t launch_pass2(const FFTPlan3& plan, const Pass2Args& a, int batch, hip
 constexpr int kRows3 = 8;
 
 #ifndef BRP_TP_ROWS
-#define BRP_TP_ROWS 24  // pass B rows per workgroup (one 24-row block of pass A's layout)
+#define BRP_TP_ROWS BRP_TP_BLOCK  // pass B rows per workgroup (one block of pass A's layout)
 #endif
 constexpr int kRowsTp = BRP_TP_ROWS;
 
 hipError_t launch_pass3(const FFTPlan3& plan, Pass3Mode mode, const Pass3Args& a, int batch, hipStream_t s) {
   if (a.tp) {
-    if (plan.L3 != 256 || a.C % 24 != 0 || mode == P3_COMPLEX) return hipErrorInvalidValue;
+    if (plan.L3 != 256 || a.C % kTpBlock != 0 || mode == P3_COMPLEX) return hipErrorInvalidValue;
     const dim3 grid((a.C / 2 + kRowsTp) / kRowsTp, batch);
     const dim3 block(2 * kRowsTp * tpc_for<256>());
     if (a.ps16) hipLaunchKernelGGL((pass3_kernel<256, kRowsTp, P3_POWER16, true>), grid, block, 0, s, a);

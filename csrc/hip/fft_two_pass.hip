@@ -13,15 +13,17 @@
 // (inputs n' >= C/3 lie in the zero padding). With c = 3 q + r (set r < 3):
 //   X_n3[3 q + r] = sum_{n'} (x[n'] W_C^{n' r}) W_8192^{n' q},
 // three 8192-point transforms of the twiddled column. Each is split as
-// n' = 16 t + j (t < 512, j < 16), q = k1 + 512 k2:
-//   Y[k1 + 512 k2] = sum_j W_16^{j k2} W_8192^{j k1} sum_t y[16 t + j] W_512^{t k1}
-// i.e. 16 LDS-resident FFT-512 columns (three radix-8 Stockham stages, the first
-// straight from the gathered registers), then per thread k1 a radix-16 DFT over
-// the 16 columns. The gathered column stays in registers across the three sets.
+// n' = 8 t + j (t < 1024, j < 8), q = k1 + 1024 k2:
+//   Y[k1 + 1024 k2] = sum_j W_8^{j k2} W_8192^{j k1} sum_t y[8 t + j] W_1024^{t k1}
+// i.e. 8 LDS-resident FFT-1024 columns (Stockham radix 16, 8, 8; the first
+// stage straight from the gathered registers), then per row k1 a radix-8 DFT
+// over the 8 columns. The gathered column stays in registers across the three
+// sets (32 VGPRs; the kernel fits 128 VGPRs without spills at two workgroups
+// per CU).
 //
 // Output layout (pass B reads it): within column n3, row c = 3 q + r is stored
-// at P(c) = 24 (q / 8) + 8 r + q % 8, so a set's 8 consecutive q are one 64-B
-// piece and rows [24 b, 24 b + 24) one 192-B block.
+// at tp_pos(c) = 24 (q / 8) + 8 r + q % 8 (kTpBlock = 24), so a set's 8
+// consecutive q are one 64-B piece and rows [24 b, 24 b + 24) one 192-B block.
 // Replaces the reference's cuFFT call and resampling kernels
 // (cuda/app/demod_binary_cuda.cu:849-965, cuda/app/demod_binary_cuda.cuh:69-184).
 #include "fft_block.hpp"
@@ -33,7 +35,8 @@ namespace hipk {
 namespace {
 
 constexpr int kAT = 512;                // threads per column workgroup
-constexpr int kACols = 16;              // FFT-512 columns (j)
+constexpr int kACols = 8;               // FFT-1024 columns (j)
+constexpr int kALen = 1024;             // FFT length per column (t)
 constexpr uint32_t kAC = 24576;         // C
 constexpr uint32_t kAL3 = 256;          // L3 (columns n3)
 constexpr uint32_t kAL2L3 = 128 * 256;  // input stride of n1
@@ -57,30 +60,30 @@ constexpr bool kAblGather = true;
 constexpr bool kAblGather = false;
 #endif
 
-// column-interleaved, XOR-swizzled 512 x 16 block: 16 lanes on one row touch
-// a permutation of its 128 B (stage reads / writes conflict-free); the final
+// column-interleaved, XOR-swizzled 1024 x 8 block: the 8 lanes of a row touch
+// a permutation of its 64 B (stage reads / writes conflict-free); the final
 // read (lanes walk rows, one column) spreads over all 64 banks
-__device__ __forceinline__ int a_idx(int t, int j) { return t * kACols + (j ^ ((t >> 1) & 15)); }
+__device__ __forceinline__ int a_idx(int t, int j) { return t * kACols + (j ^ ((t >> 2) & 7)); }
 
-// radix-8 Stockham stage (Ns > 1) of the 16 FFT-512 columns, LDS -> LDS:
-// butterflies j' = tj, tj + 32 of column c
+// radix-8 Stockham stage (Ns = 16, 128) of the 8 FFT-1024 columns, LDS -> LDS:
+// butterflies j' = tj, tj + 64 of column c
 template <int Ns>
-__device__ __forceinline__ void a_stage(float2* data, const float2* w512, int c, int tj) {
+__device__ __forceinline__ void a_stage(float2* data, const float2* w1024, int c, int tj) {
   float2 v[2][8];
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
-    const int jp = tj + 32 * h;
+    const int jp = tj + 64 * h;
 #pragma unroll
-    for (int p = 0; p < 8; ++p) v[h][p] = data[a_idx(jp + 64 * p, c)];
+    for (int p = 0; p < 8; ++p) v[h][p] = data[a_idx(jp + 128 * p, c)];
     const int jm = jp % Ns;
 #pragma unroll
-    for (int p = 1; p < 8; ++p) v[h][p] = cmul(v[h][p], w512[(jm * p * (512 / (8 * Ns))) & 511]);
-    Dft<8>::run(v[h]);
+    for (int p = 1; p < 8; ++p) v[h][p] = cmul(v[h][p], w1024[(jm * p * (kALen / (8 * Ns))) & (kALen - 1)]);
+    if constexpr (!kAblFft) Dft<8>::run(v[h]);
   }
   __syncthreads();
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
-    const int jp = tj + 32 * h;
+    const int jp = tj + 64 * h;
     const int base = (jp / Ns) * Ns * 8 + (jp % Ns);
 #pragma unroll
     for (int p = 0; p < 8; ++p) data[a_idx(base + Ns * p, c)] = v[h][p];
@@ -89,24 +92,22 @@ __device__ __forceinline__ void a_stage(float2* data, const float2* w512, int c,
 }
 
 __global__ void __launch_bounds__(kAT) __attribute__((amdgpu_waves_per_eu(4, 8))) pass_a_kernel(PassAArgs a) {
-  __shared__ __attribute__((aligned(16))) float2 data[512 * kACols];
-  __shared__ float2 w512[512];           // W_512^e
+  __shared__ __attribute__((aligned(16))) float2 data[kALen * kACols];
+  __shared__ float2 w1024[kALen];        // W_1024^e
   __shared__ float2 w48[48];             // W_48^e  (= W_C^{512 e})
-  __shared__ float2 wk2[16];             // W_M^{1536 n3 k2}
+  __shared__ float2 wk2[8];              // W_M^{3072 n3 k2}
   __shared__ float lut_s[kLutSize], lut_c[kLutSize];
   __shared__ double red[kAT / kWave + 1];
 
   const int b = blockIdx.y;
   const uint32_t n3 = xcd_remap(blockIdx.x, gridDim.x);  // neighbouring columns share series lines: one XCD
   const int tid = static_cast<int>(threadIdx.x);
-  const int c = tid % kACols;  // FFT column j (stages) / gathered n' residue
-  const int tj = tid / kACols;
   if (a.reset != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && tid == 0) *a.reset = 0;
 
   const TemplateDev td = a.tmpl[b];
   // tables: issued together ahead of the gather
   {
-    const float2 v = a.w512[tid];
+    const float2 v0 = a.w1024[tid], v1 = a.w1024[tid + kAT];
     float ls = 0.0f, lc = 0.0f;
     if (tid < kLutSize) {
       ls = kSinLut[tid];
@@ -114,18 +115,22 @@ __global__ void __launch_bounds__(kAT) __attribute__((amdgpu_waves_per_eu(4, 8))
     }
     float2 v48 = make_float2(0.f, 0.f), vk = v48;
     if (tid < 48) v48 = a.w48[tid];
-    if (tid >= 64 && tid < 80) vk = tw_lookup(a.tw, 4ull * 1536u * n3 * static_cast<uint32_t>(tid - 64));
-    w512[tid] = v;
+    if (tid >= 64 && tid < 72) vk = tw_lookup(a.tw, 4ull * 3072u * n3 * static_cast<uint32_t>(tid - 64));
+    w1024[tid] = v0;
+    w1024[tid + kAT] = v1;
     if (tid < kLutSize) {
       lut_s[tid] = ls;
       lut_c[tid] = lc;
     }
     if (tid < 48) w48[tid] = v48;
-    if (tid >= 64 && tid < 80) wk2[tid - 64] = vk;
+    if (tid >= 64 && tid < 72) wk2[tid - 64] = vk;
   }
   __syncthreads();
 
-  // gather rows t = tj + 32 u of column j = c: n' = 16 t + c -> n1 = n' / 128, n2 = n' % 128
+  // gather rows t = tj + 64 u (u < 16) of column j = c: n' = 8 t + c ->
+  // n1 = n' / 128, n2 = n' % 128 (complex sample 256 n' + n3)
+  const int c0 = tid % kACols;
+  const int tj0 = tid / kACols;
   const bool fast = a.n_unpadded <= (1u << 23);
   const float* series = a.series + static_cast<size_t>(td.wu) * a.n_unpadded;
   const int last = static_cast<int>(a.n_unpadded) - 1;
@@ -138,7 +143,7 @@ __global__ void __launch_bounds__(kAT) __attribute__((amdgpu_waves_per_eu(4, 8))
 #pragma unroll
     for (int v = 0; v < 8; ++v) {
       const int u = 8 * hf + v;
-      const uint32_t np = 16u * (tj + 32u * u) + c;
+      const uint32_t np = 8u * (tj0 + 64u * u) + c0;
       const uint32_t m0 = 2u * ((np >> 7) * kAL2L3 + (np & 127u) * kAL3 + n3);
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
@@ -167,6 +172,7 @@ __global__ void __launch_bounds__(kAT) __attribute__((amdgpu_waves_per_eu(4, 8))
     }
   }
 
+  // output origin, uniform: kept in SGPRs (stores are SGPR base + lane offset)
   char* outb;
   {
     const uint64_t o = reinterpret_cast<uint64_t>(a.out + (static_cast<size_t>(b) * kAL3 + n3) * kAC);
@@ -175,68 +181,60 @@ __global__ void __launch_bounds__(kAT) __attribute__((amdgpu_waves_per_eu(4, 8))
   }
 #pragma unroll 1
   for (int r = 0; r < 3; ++r) {
-    // thread coordinates made opaque per set: otherwise the ~80 LDS addresses
-    // of the set are hoisted out of the loop and held in registers (spills)
+    // thread coordinates made opaque per set: otherwise the set's LDS
+    // addresses are hoisted out of the loop and held in registers
     int tr = tid;
     asm volatile("" : "+v"(tr));
-    const int c = tr % kACols, tj = tr / kACols, k1 = tr;
-    // set twiddle base W_C^{(16 tj + c) r} (W_4M^{1024 e}); looked up per set
-    // (a table read) rather than held across the sets
-    const float2 ar = tw_lookup32(a.tw, 1024u * r * (16u * tj + c));
-    // set twiddle y = x W_C^{(16 t + j) r} = x * W_C^{e0 r} * W_48^{u r}; stage 1
-    // (radix 8, Ns = 1) in registers: butterfly j' = tj (rows t = tj + 64 p,
-    // u = 2 p) and j' = tj + 32 (u = 2 p + 1)
-    float2 v[2][8];
+    const int c = tr % kACols, tj = tr / kACols;
+    // set twiddle y = x W_C^{(8 t + j) r} = x * W_C^{(8 tj + c) r} * W_48^{u r}
+    // (W_C^e = W_4M^{1024 e}); stage 1 (radix 16, Ns = 1) in registers:
+    // butterfly j' = tj reads rows t = tj + 64 u, exactly the gathered ones
+    const float2 ar = tw_lookup32(a.tw, 1024u * r * (8u * tj + c));
+    float2 v[16];
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      float2 y = x[u];
-      if (r != 0) y = cmul(y, u == 0 ? ar : cmul(ar, w48[(u * r) % 48]));
-      v[u & 1][u >> 1] = y;
-    }
-    if constexpr (!kAblFft) {
-      Dft<8>::run(v[0]);
-      Dft<8>::run(v[1]);
-    }
+    for (int u = 0; u < 16; ++u) v[u] = (r == 0) ? x[u] : cmul(x[u], u == 0 ? ar : cmul(ar, w48[(u * r) % 48]));
+    if constexpr (!kAblFft) Dft<16>::run(v);
     if (r != 0) __syncthreads();  // the previous set's final reads are done
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int jp = tj + 32 * h;
-#pragma unroll
-      for (int p = 0; p < 8; ++p) data[a_idx(8 * jp + p, c)] = v[h][p];
-    }
+    for (int p = 0; p < 16; ++p) data[a_idx(16 * tj + p, c)] = v[p];
     __syncthreads();
     if constexpr (!kAblFft) {
-      a_stage<8>(data, w512, c, tj);
-      a_stage<64>(data, w512, c, tj);
+      a_stage<16>(data, w1024, c, tj);
+      a_stage<128>(data, w1024, c, tj);
     }
-    // final: row k1 of the 16 columns, twiddle W_8192^{j k1}, radix 16 over j -> k2
-    float2 wp[4];  // W_8192^{k1 2^i} (W_4M^{3072 e})
+    // final: rows k1 = tid, tid + 512 of the 8 columns, twiddle W_8192^{j k1},
+    // radix 8 over j -> k2; q = k1 + 1024 k2, c = 3 q + r
+    constexpr uint32_t kQb = kTpBlock / 3;  // q per layout block
 #pragma unroll
-    for (int i = 0; i < 4; ++i) wp[i] = tw_lookup32(a.tw, (3072u << i) * static_cast<uint32_t>(k1));
-    float2 z[16];
+    for (int hh = 0; hh < 2; ++hh) {
+      const int k1 = tr + kAT * hh;
+      float2 z[8];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) z[j] = data[a_idx(k1, j)];
+      for (int j = 0; j < 8; ++j) z[j] = data[a_idx(k1, j)];
+      float2 wp[3];  // W_8192^{k1 2^i} (W_4M^{3072 e}), exact table products
 #pragma unroll
-    for (int j = 1; j < 16; ++j) {
-      float2 w = make_float2(1.f, 0.f);
-      bool first = true;
+      for (int i = 0; i < 3; ++i) wp[i] = tw_lookup32(a.tw, (3072u << i) * static_cast<uint32_t>(k1));
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        if (j & (1 << i)) {
-          w = first ? wp[i] : cmul(w, wp[i]);
-          first = false;
-        }
-      z[j] = cmul(z[j], w);
-    }
-    if constexpr (!kAblFft) Dft<16>::run(z);
-    // output twiddle W_M^{n3 c}, c = 3 (k1 + 512 k2) + r = (3 k1 + r) + 1536 k2
-    const float2 wo = tw_lookup32(a.tw, 4u * n3 * (3u * k1 + r));
-    // stores: one uniform (SGPR) origin + a 32-bit lane offset stepped by k2
-    uint32_t off = (24u * (k1 >> 3) + 8u * r + (k1 & 7)) * sizeof(float2);
+      for (int j = 1; j < 8; ++j) {
+        float2 w = make_float2(1.f, 0.f);
+        bool first = true;
 #pragma unroll
-    for (int k2 = 0; k2 < 16; ++k2) {
-      *reinterpret_cast<float2*>(outb + off) = cmul(z[k2], cmul(wo, wk2[k2]));
-      off += 1536u * sizeof(float2);
+        for (int i = 0; i < 3; ++i)
+          if (j & (1 << i)) {
+            w = first ? wp[i] : cmul(w, wp[i]);
+            first = false;
+          }
+        z[j] = cmul(z[j], w);
+      }
+      if constexpr (!kAblFft) Dft<8>::run(z);
+      // output twiddle W_M^{n3 c} = W_M^{n3 (3 k1 + r)} W_M^{3072 n3 k2}
+      const float2 wo = tw_lookup32(a.tw, 4u * n3 * (3u * k1 + r));
+      uint32_t off = (kTpBlock * (k1 / kQb) + kQb * r + (k1 % kQb)) * sizeof(float2);
+#pragma unroll
+      for (int k2 = 0; k2 < 8; ++k2) {
+        *reinterpret_cast<float2*>(outb + off) = cmul(z[k2], cmul(wo, wk2[k2]));
+        off += 3072u * sizeof(float2);  // q + 1024: 1024 / kQb blocks
+      }
     }
   }
   const double tot = block_sum<kAT>(static_cast<double>(fsum), red);
