@@ -994,6 +994,10 @@ hipError_t launch_pass2(const FFTPlan3& plan, const Pass2Args& a, int batch, hip
 }
 
 constexpr int kRows3 = 8;
+#ifndef BRP_P3_ROWS
+#define BRP_P3_ROWS 8  // untangle pass: own rows per workgroup (build switch, profiles/README.md)
+#endif
+constexpr int kRowsP = BRP_P3_ROWS;
 
 #ifndef BRP_TP_ROWS
 #define BRP_TP_ROWS BRP_TP_BLOCK  // pass B rows per workgroup (one block of pass A's layout)
@@ -1010,15 +1014,16 @@ hipError_t launch_pass3(const FFTPlan3& plan, Pass3Mode mode, const Pass3Args& a
     return hipGetLastError();
   }
   if (plan.rows3 != kRows3) return hipErrorInvalidValue;
-  const dim3 grid(plan.wg3(), batch);
+  // rows per workgroup of the untangle pass (own rows; as many mirror rows)
+  const dim3 grid(((plan.L1 * plan.L2) / 2 + kRowsP) / kRowsP, batch);
   switch (plan.L3) {
 #define X(n)                                                                                              \
   case n: {                                                                                               \
-    const dim3 block(2 * kRows3 * tpc_for<n>());                                                          \
+    const dim3 block(2 * kRowsP * tpc_for<n>());                                                          \
     if (mode == P3_POWER && a.ps16)                                                                       \
-      hipLaunchKernelGGL((pass3_kernel<n, kRows3, P3_POWER16>), grid, block, 0, s, a);                    \
-    else if (mode == P3_POWER) hipLaunchKernelGGL((pass3_kernel<n, kRows3, P3_POWER>), grid, block, 0, s, a); \
-    else hipLaunchKernelGGL((pass3_kernel<n, kRows3, P3_COMPLEX>), grid, block, 0, s, a);                 \
+      hipLaunchKernelGGL((pass3_kernel<n, kRowsP, P3_POWER16>), grid, block, 0, s, a);                    \
+    else if (mode == P3_POWER) hipLaunchKernelGGL((pass3_kernel<n, kRowsP, P3_POWER>), grid, block, 0, s, a); \
+    else hipLaunchKernelGGL((pass3_kernel<n, kRowsP, P3_COMPLEX>), grid, block, 0, s, a);                 \
     break;                                                                                                \
   }
     BRP_P3_LENGTHS(X)
