@@ -486,6 +486,7 @@ struct HipEngine::Impl {
   }
   DevBuf<float2> t_st1, t_st2, t_st3, t_p1, t_p2col, t_p2lo, t_p2hi, t_p3;
   DevBuf<float2> t_a1024, t_a48;
+  DevBuf<float> t_lut;  // kSinLut | kCosLut (pass A reads the LUT through the caches)
   // Two-pass plan for the benchmark geometry (fft_two_pass.hip): pass A = the
   // resampling gather and the whole 24576-point column transform, pass B =
   // pass 3 on transposed row tiles; 100 MB less memory traffic per template
@@ -531,6 +532,11 @@ struct HipEngine::Impl {
         (rc = upload(t_p2hi, h.p2hi)) || (rc = upload(t_p3, h.p3)) || (rc = upload(t_a1024, h.a1024)) ||
         (rc = upload(t_a48, h.a48)))
       return rc;
+    std::vector<float> lut(kSinLut, kSinLut + kLutSize);
+    lut.insert(lut.end(), kCosLut, kCosLut + kLutSize);
+    if ((rc = t_lut.alloc(lut.size()))) return rc;
+    if (copy_sync(t_lut.p, lut.data(), lut.size() * sizeof(float), hipMemcpyHostToDevice, stream) != hipSuccess)
+      return RADPUL_HIP_MEM_COPY_HOST_DEVICE;
     return 0;
   }
 
@@ -698,6 +704,8 @@ struct HipEngine::Impl {
       aa.tw = tw;
       aa.w1024 = t_a1024.p;
       aa.w48 = t_a48.p;
+      aa.lut_sin = t_lut.p;
+      aa.lut_cos = t_lut.p + kLutSize;
       aa.series = series_in();
       aa.n_unpadded = g.n_unpadded;
       aa.tmpl = tmpl.p;

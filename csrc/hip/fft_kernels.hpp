@@ -142,6 +142,8 @@ struct PassAArgs {
   TwiddleTable tw;             // W_2N (N = fft size)
   const float2* w1024;         // W_1024^e, e < 1024
   const float2* w48;           // W_48^e, e < 48
+  const float* lut_sin;        // sine / cosine LUT of the resampling (kSinLut, kCosLut)
+  const float* lut_cos;
   const float* series;         // [slots][n_unpadded]
   uint32_t n_unpadded;
   const TemplateDev* tmpl;     // [batch]

@@ -1000,7 +1000,7 @@ constexpr int kRows3 = 8;
 constexpr int kRowsP = BRP_P3_ROWS;
 
 #ifndef BRP_TP_ROWS
-#define BRP_TP_ROWS BRP_TP_BLOCK  // pass B rows per workgroup (one block of pass A's layout)
+#define BRP_TP_ROWS 8  // pass B rows per workgroup (32 KB of LDS; 24 = one layout block, 96 KB)
 #endif
 constexpr int kRowsTp = BRP_TP_ROWS;
 

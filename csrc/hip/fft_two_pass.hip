@@ -68,7 +68,7 @@ __device__ __forceinline__ int a_idx(int t, int j) { return t * kACols + (j ^ ((
 // radix-8 Stockham stage (Ns = 16, 128) of the 8 FFT-1024 columns, LDS -> LDS:
 // butterflies j' = tj, tj + 64 of column c
 template <int Ns>
-__device__ __forceinline__ void a_stage(float2* data, const float2* w1024, int c, int tj) {
+__device__ __forceinline__ void a_stage(float2* data, const float2* __restrict__ w1024, int c, int tj) {
   float2 v[2][8];
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
@@ -91,13 +91,14 @@ __device__ __forceinline__ void a_stage(float2* data, const float2* w1024, int c
   __syncthreads();
 }
 
+// LDS: exactly the 64 KB column block (the twiddle tables and the sine LUT are
+// read through the caches; the block-sum scratch reuses the block at the end)
 __global__ void __launch_bounds__(kAT) __attribute__((amdgpu_waves_per_eu(4, 8))) pass_a_kernel(PassAArgs a) {
   __shared__ __attribute__((aligned(16))) float2 data[kALen * kACols];
-  __shared__ float2 w1024[kALen];        // W_1024^e
-  __shared__ float2 w48[48];             // W_48^e  (= W_C^{512 e})
-  __shared__ float2 wk2[8];              // W_M^{3072 n3 k2}
-  __shared__ float lut_s[kLutSize], lut_c[kLutSize];
-  __shared__ double red[kAT / kWave + 1];
+  const float2* __restrict__ w1024 = a.w1024;  // W_1024^e
+  const float2* __restrict__ w48 = a.w48;      // W_48^e  (= W_C^{512 e})
+  const float* __restrict__ lut_s = a.lut_sin;
+  const float* __restrict__ lut_c = a.lut_cos;
 
   const int b = blockIdx.y;
   const uint32_t n3 = xcd_remap(blockIdx.x, gridDim.x);  // neighbouring columns share series lines: one XCD
@@ -105,28 +106,6 @@ __global__ void __launch_bounds__(kAT) __attribute__((amdgpu_waves_per_eu(4, 8))
   if (a.reset != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && tid == 0) *a.reset = 0;
 
   const TemplateDev td = a.tmpl[b];
-  // tables: issued together ahead of the gather
-  {
-    const float2 v0 = a.w1024[tid], v1 = a.w1024[tid + kAT];
-    float ls = 0.0f, lc = 0.0f;
-    if (tid < kLutSize) {
-      ls = kSinLut[tid];
-      lc = kCosLut[tid];
-    }
-    float2 v48 = make_float2(0.f, 0.f), vk = v48;
-    if (tid < 48) v48 = a.w48[tid];
-    if (tid >= 64 && tid < 72) vk = tw_lookup(a.tw, 4ull * 3072u * n3 * static_cast<uint32_t>(tid - 64));
-    w1024[tid] = v0;
-    w1024[tid + kAT] = v1;
-    if (tid < kLutSize) {
-      lut_s[tid] = ls;
-      lut_c[tid] = lc;
-    }
-    if (tid < 48) w48[tid] = v48;
-    if (tid >= 64 && tid < 72) wk2[tid - 64] = vk;
-  }
-  __syncthreads();
-
   // gather rows t = tj + 64 u (u < 16) of column j = c: n' = 8 t + c ->
   // n1 = n' / 128, n2 = n' % 128 (complex sample 256 n' + n3)
   const int c0 = tid % kACols;
@@ -232,12 +211,15 @@ __global__ void __launch_bounds__(kAT) __attribute__((amdgpu_waves_per_eu(4, 8))
       uint32_t off = (kTpBlock * (k1 / kQb) + kQb * r + (k1 % kQb)) * sizeof(float2);
 #pragma unroll
       for (int k2 = 0; k2 < 8; ++k2) {
-        *reinterpret_cast<float2*>(outb + off) = cmul(z[k2], cmul(wo, wk2[k2]));
+        // W_M^{3072 n3 k2}: a uniform exponent (scalar-cache table reads)
+        const float2 wk = tw_lookup(a.tw, 4ull * 3072u * n3 * static_cast<uint32_t>(k2));
+        *reinterpret_cast<float2*>(outb + off) = cmul(z[k2], cmul(wo, wk));
         off += 3072u * sizeof(float2);  // q + 1024: 1024 / kQb blocks
       }
     }
   }
-  const double tot = block_sum<kAT>(static_cast<double>(fsum), red);
+  // block_sum's first barrier orders the scratch writes after the last reads of the block
+  const double tot = block_sum<kAT>(static_cast<double>(fsum), reinterpret_cast<double*>(data));
   if (tid == 0) a.partials[static_cast<size_t>(b) * gridDim.x + blockIdx.x] = tot;
 }
 
