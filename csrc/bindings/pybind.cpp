@@ -21,6 +21,7 @@
 #include "../core/rngmed.hpp"
 #include "../core/search_core.hpp"
 #include "../core/stats.hpp"
+#include "../hip/two_pass_check.hpp"
 #include "../core/wisdom.hpp"
 #include "../engine/hip_engine.hpp"
 
@@ -532,6 +533,8 @@ PYBIND11_MODULE(_brp, m) {
     if (!make_fft_plan(M, p)) return py::none();
     return py::make_tuple(p.L1, p.L2, p.L3);
   });
+  m.def("two_pass_selftest", [] { return hipk::two_pass_selftest(); },
+        "host-side check of the two-pass plan's index algebra (\"\" = ok)");
   m.def("bluestein_plan", [](uint32_t Mb) -> py::object {
     FFTPlan3 p;
     if (!make_bluestein_plan(Mb, p)) return py::none();

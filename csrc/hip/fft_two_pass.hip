@@ -26,8 +26,12 @@
 // consecutive q are one 64-B piece and rows [24 b, 24 b + 24) one 192-B block.
 // Replaces the reference's cuFFT call and resampling kernels
 // (cuda/app/demod_binary_cuda.cu:849-965, cuda/app/demod_binary_cuda.cuh:69-184).
+#include <string>
+#include <vector>
+
 #include "fft_block.hpp"
 #include "fft_kernels.hpp"
+#include "two_pass_check.hpp"
 
 namespace brp {
 namespace hipk {
@@ -63,7 +67,16 @@ constexpr bool kAblGather = false;
 // column-interleaved, XOR-swizzled 1024 x 8 block: the 8 lanes of a row touch
 // a permutation of its 64 B (stage reads / writes conflict-free); the final
 // read (lanes walk rows, one column) spreads over all 64 banks
-__device__ __forceinline__ int a_idx(int t, int j) { return t * kACols + (j ^ ((t >> 2) & 7)); }
+__host__ __device__ inline int a_idx(int t, int j) { return t * kACols + (j ^ ((t >> 2) & 7)); }
+
+// pass A's output position of (set r, row k1, output k2) within a column:
+// q = k1 + 1024 k2, c = 3 q + r, tp_pos(c)
+__host__ __device__ inline uint32_t pa_store_pos(uint32_t r, uint32_t k1, uint32_t k2) {
+  constexpr uint32_t kQb = kTpBlock / 3;  // q per layout block
+  return kTpBlock * (k1 / kQb) + kQb * r + (k1 % kQb) + 3072u * k2;  // q + 1024: 1024 / kQb blocks
+}
+// Stockham row written by stage (radix R, span Ns) for butterfly jp, output p
+__host__ __device__ inline int a_stage_row(int Ns, int R, int jp, int p) { return (jp / Ns) * Ns * R + (jp % Ns) + Ns * p; }
 
 // radix-8 Stockham stage (Ns = 16, 128) of the 8 FFT-1024 columns, LDS -> LDS:
 // butterflies j' = tj, tj + 64 of column c
@@ -84,9 +97,8 @@ __device__ __forceinline__ void a_stage(float2* data, const float2* __restrict__
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const int jp = tj + 64 * h;
-    const int base = (jp / Ns) * Ns * 8 + (jp % Ns);
 #pragma unroll
-    for (int p = 0; p < 8; ++p) data[a_idx(base + Ns * p, c)] = v[h][p];
+    for (int p = 0; p < 8; ++p) data[a_idx(a_stage_row(Ns, 8, jp, p), c)] = v[h][p];
   }
   __syncthreads();
 }
@@ -175,7 +187,7 @@ __global__ void __launch_bounds__(kAT) __attribute__((amdgpu_waves_per_eu(4, 8))
     if constexpr (!kAblFft) Dft<16>::run(v);
     if (r != 0) __syncthreads();  // the previous set's final reads are done
 #pragma unroll
-    for (int p = 0; p < 16; ++p) data[a_idx(16 * tj + p, c)] = v[p];
+    for (int p = 0; p < 16; ++p) data[a_idx(a_stage_row(1, 16, tj, p), c)] = v[p];
     __syncthreads();
     if constexpr (!kAblFft) {
       a_stage<16>(data, w1024, c, tj);
@@ -183,7 +195,6 @@ __global__ void __launch_bounds__(kAT) __attribute__((amdgpu_waves_per_eu(4, 8))
     }
     // final: rows k1 = tid, tid + 512 of the 8 columns, twiddle W_8192^{j k1},
     // radix 8 over j -> k2; q = k1 + 1024 k2, c = 3 q + r
-    constexpr uint32_t kQb = kTpBlock / 3;  // q per layout block
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {
       const int k1 = tr + kAT * hh;
@@ -208,13 +219,13 @@ __global__ void __launch_bounds__(kAT) __attribute__((amdgpu_waves_per_eu(4, 8))
       if constexpr (!kAblFft) Dft<8>::run(z);
       // output twiddle W_M^{n3 c} = W_M^{n3 (3 k1 + r)} W_M^{3072 n3 k2}
       const float2 wo = tw_lookup32(a.tw, 4u * n3 * (3u * k1 + r));
-      uint32_t off = (kTpBlock * (k1 / kQb) + kQb * r + (k1 % kQb)) * sizeof(float2);
+      uint32_t off = pa_store_pos(r, k1, 0) * sizeof(float2);
 #pragma unroll
       for (int k2 = 0; k2 < 8; ++k2) {
         // W_M^{3072 n3 k2}: a uniform exponent (scalar-cache table reads)
         const float2 wk = tw_lookup(a.tw, 4ull * 3072u * n3 * static_cast<uint32_t>(k2));
         *reinterpret_cast<float2*>(outb + off) = cmul(z[k2], cmul(wo, wk));
-        off += 3072u * sizeof(float2);  // q + 1024: 1024 / kQb blocks
+        off += (pa_store_pos(0, 0, 1) - pa_store_pos(0, 0, 0)) * sizeof(float2);
       }
     }
   }
@@ -224,6 +235,44 @@ __global__ void __launch_bounds__(kAT) __attribute__((amdgpu_waves_per_eu(4, 8))
 }
 
 }  // namespace
+
+std::string two_pass_selftest() {
+  // pass A stores: a permutation of the column, and the inverse of tp_pos
+  std::vector<uint8_t> seen(kAC, 0);
+  for (uint32_t r = 0; r < 3; ++r)
+    for (uint32_t k1 = 0; k1 < static_cast<uint32_t>(kALen); ++k1)
+      for (uint32_t k2 = 0; k2 < 8; ++k2) {
+        const uint32_t pos = pa_store_pos(r, k1, k2);
+        if (pos >= kAC) return "pass A store position out of the column";
+        if (seen[pos]++) return "pass A store position written twice";
+        if (tp_pos(3u * (k1 + 1024u * k2) + r) != pos) return "tp_pos is not pass A's layout";
+      }
+  // LDS block: a_idx is a permutation of the 1024 x 8 block
+  std::vector<uint8_t> lds(kALen * kACols, 0);
+  for (int t = 0; t < kALen; ++t)
+    for (int j = 0; j < kACols; ++j) {
+      const int e = a_idx(t, j);
+      if (e < 0 || e >= kALen * kACols || lds[e]++) return "a_idx is not a permutation";
+    }
+  // Stockham stages 16 x 8 x 8: each writes every row of a column once
+  const int stages[3][2] = {{1, 16}, {16, 8}, {128, 8}};
+  for (const auto& st : stages) {
+    std::vector<uint8_t> rows(kALen, 0);
+    for (int jp = 0; jp < kALen / st[1]; ++jp)
+      for (int p = 0; p < st[1]; ++p) {
+        const int row = a_stage_row(st[0], st[1], jp, p);
+        if (row < 0 || row >= kALen || rows[row]++) return "Stockham stage rows";
+      }
+  }
+  // pass B tiles: every row a workgroup loads maps into the column
+  for (uint32_t blk = 0; blk < (kAC / 2 + 24) / 8; ++blk)
+    for (uint32_t s = 0; s < 64; ++s) {
+      const uint32_t cs = blk * 8 + (s % 32);
+      const uint32_t row = s < 32 ? cs : (kAC - cs) % kAC;
+      if (tp_pos(row < kAC ? row : 0) >= kAC) return "pass B row outside the column";
+    }
+  return "";
+}
 
 bool two_pass_supported(const FFTPlan3& plan, uint32_t n_unpadded) {
   return plan.L1 * plan.L2 == kAC && plan.L3 == kAL3 && plan.L2 * plan.L3 == kAL2L3 &&
