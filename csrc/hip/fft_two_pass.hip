@@ -164,11 +164,16 @@ __global__ void __launch_bounds__(kAT) __attribute__((amdgpu_waves_per_eu(4, 8))
   }
 
   // output origin, uniform: kept in SGPRs (stores are SGPR base + lane offset)
+  // (readfirstlane returns a signed int: each half goes back through uint32_t
+  // before widening, or a low half >= 2^31 would sign-extend over the high half
+  // -- the out-of-range stores the first forms of this kernel made whenever the
+  // column's address had bit 31 set, profiles/two_pass_r4.txt)
   char* outb;
   {
     const uint64_t o = reinterpret_cast<uint64_t>(a.out + (static_cast<size_t>(b) * kAL3 + n3) * kAC);
-    outb = reinterpret_cast<char*>((static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(o >> 32))) << 32) |
-                                   __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(o)));
+    const uint32_t lo = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(static_cast<uint32_t>(o))));
+    const uint32_t hi = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(static_cast<uint32_t>(o >> 32))));
+    outb = reinterpret_cast<char*>((static_cast<uint64_t>(hi) << 32) | lo);
   }
 #pragma unroll 1
   for (int r = 0; r < 3; ++r) {
