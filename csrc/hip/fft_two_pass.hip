@@ -44,6 +44,14 @@ constexpr int kALen = 1024;             // FFT length per column (t)
 constexpr uint32_t kAC = 24576;         // C
 constexpr uint32_t kAL3 = 256;          // L3 (columns n3)
 constexpr uint32_t kAL2L3 = 128 * 256;  // input stride of n1
+// neighbouring columns per workgroup (build switch): 2 halves the series lines
+// the column gathers fetch per column (a line holds 16 columns), at one
+// workgroup per CU instead of two
+#ifndef BRP_PA_COLS
+#define BRP_PA_COLS 1
+#endif
+constexpr int kNC = BRP_PA_COLS;
+static_assert(kNC == 1 || kNC == 2, "columns per pass-A workgroup");
 
 // Speed-of-light ablations for experiment builds (scripts/build_variant.sh,
 // wrong results): BRP_ABLATE_PA_RES drops the resampling arithmetic,
@@ -105,7 +113,7 @@ __device__ __forceinline__ void a_stage(float2* data, const float2* __restrict__
 
 // LDS: exactly the 64 KB column block (the twiddle tables and the sine LUT are
 // read through the caches; the block-sum scratch reuses the block at the end)
-__global__ void __launch_bounds__(kAT) __attribute__((amdgpu_waves_per_eu(4, 8))) pass_a_kernel(PassAArgs a) {
+__global__ void __launch_bounds__(kAT) __attribute__((amdgpu_waves_per_eu(kNC == 1 ? 4 : 2, 8))) pass_a_kernel(PassAArgs a) {
   __shared__ __attribute__((aligned(16))) float2 data[kALen * kACols];
   const float2* __restrict__ w1024 = a.w1024;  // W_1024^e
   const float2* __restrict__ w48 = a.w48;      // W_48^e  (= W_C^{512 e})
@@ -113,7 +121,7 @@ __global__ void __launch_bounds__(kAT) __attribute__((amdgpu_waves_per_eu(4, 8))
   const float* __restrict__ lut_c = a.lut_cos;
 
   const int b = blockIdx.y;
-  const uint32_t n3 = xcd_remap(blockIdx.x, gridDim.x);  // neighbouring columns share series lines: one XCD
+  const uint32_t n3b = kNC * xcd_remap(blockIdx.x, gridDim.x);  // neighbouring columns share series lines: one XCD
   const int tid = static_cast<int>(threadIdx.x);
   if (a.reset != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && tid == 0) *a.reset = 0;
 
@@ -126,19 +134,18 @@ __global__ void __launch_bounds__(kAT) __attribute__((amdgpu_waves_per_eu(4, 8))
   const float* series = a.series + static_cast<size_t>(td.wu) * a.n_unpadded;
   const int last = static_cast<int>(a.n_unpadded) - 1;
   float fsum = 0.0f;
-  float2 x[16];
-  // two halves of 8 rows (16 indices and loads in flight each): bounded registers
+  float2 x[kNC][16];
+  // two halves of 8 rows (16 indices and loads in flight each, per column)
 #pragma unroll
   for (int hf = 0; hf < 2; ++hf) {
-    int idx[16];
+    int idx[kNC][16];
 #pragma unroll
     for (int v = 0; v < 8; ++v) {
       const int u = 8 * hf + v;
       const uint32_t np = 8u * (tj0 + 64u * u) + c0;
-      const uint32_t m0 = 2u * ((np >> 7) * kAL2L3 + (np & 127u) * kAL3 + n3);
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const uint32_t m = m0 + h;
+      for (int h = 0; h < 2 * kNC; ++h) {  // samples m0 .. m0 + 2 kNC - 1: the columns' pairs, adjacent
+        const uint32_t m = 2u * ((np >> 7) * kAL2L3 + (np & 127u) * kAL3 + n3b) + h;
         int i = -1;
         if (m < td.n_steps) {
           if constexpr (kAblRes) {
@@ -148,18 +155,22 @@ __global__ void __launch_bounds__(kAT) __attribute__((amdgpu_waves_per_eu(4, 8))
             i = min(max(fast ? resamp_nearest_f(m, dt) : resamp_nearest(m, dt), 0), last);
           }
         }
-        idx[2 * v + h] = i;
+        idx[h >> 1][2 * v + (h & 1)] = i;
       }
     }
-    float raw[16];
 #pragma unroll
-    for (int e = 0; e < 16; ++e) raw[e] = kAblGather ? static_cast<float>(idx[e]) : series[idx[e] < 0 ? 0 : idx[e]];
+    for (int cc = 0; cc < kNC; ++cc) {
+      float raw[16];
 #pragma unroll
-    for (int v = 0; v < 8; ++v) {
-      const float x0 = idx[2 * v] < 0 ? 0.0f : raw[2 * v] - td.mu0;
-      const float x1 = idx[2 * v + 1] < 0 ? 0.0f : raw[2 * v + 1] - td.mu0;
-      fsum += x0 + x1;
-      x[8 * hf + v] = make_float2(x0, x1);
+      for (int e = 0; e < 16; ++e)
+        raw[e] = kAblGather ? static_cast<float>(idx[cc][e]) : series[idx[cc][e] < 0 ? 0 : idx[cc][e]];
+#pragma unroll
+      for (int v = 0; v < 8; ++v) {
+        const float x0 = idx[cc][2 * v] < 0 ? 0.0f : raw[2 * v] - td.mu0;
+        const float x1 = idx[cc][2 * v + 1] < 0 ? 0.0f : raw[2 * v + 1] - td.mu0;
+        fsum += x0 + x1;
+        x[cc][8 * hf + v] = make_float2(x0, x1);
+      }
     }
   }
 
@@ -168,6 +179,9 @@ __global__ void __launch_bounds__(kAT) __attribute__((amdgpu_waves_per_eu(4, 8))
   // before widening, or a low half >= 2^31 would sign-extend over the high half
   // -- the out-of-range stores the first forms of this kernel made whenever the
   // column's address had bit 31 set, profiles/two_pass_r4.txt)
+#pragma unroll 1
+  for (int cc = 0; cc < kNC; ++cc) {
+  const uint32_t n3 = n3b + cc;
   char* outb;
   {
     const uint64_t o = reinterpret_cast<uint64_t>(a.out + (static_cast<size_t>(b) * kAL3 + n3) * kAC);
@@ -188,9 +202,9 @@ __global__ void __launch_bounds__(kAT) __attribute__((amdgpu_waves_per_eu(4, 8))
     const float2 ar = tw_lookup32(a.tw, 1024u * r * (8u * tj + c));
     float2 v[16];
 #pragma unroll
-    for (int u = 0; u < 16; ++u) v[u] = (r == 0) ? x[u] : cmul(x[u], u == 0 ? ar : cmul(ar, w48[(u * r) % 48]));
+    for (int u = 0; u < 16; ++u) v[u] = (r == 0) ? x[cc][u] : cmul(x[cc][u], u == 0 ? ar : cmul(ar, w48[(u * r) % 48]));
     if constexpr (!kAblFft) Dft<16>::run(v);
-    if (r != 0) __syncthreads();  // the previous set's final reads are done
+    if (r != 0 || cc != 0) __syncthreads();  // the previous set's final reads are done
 #pragma unroll
     for (int p = 0; p < 16; ++p) data[a_idx(a_stage_row(1, 16, tj, p), c)] = v[p];
     __syncthreads();
@@ -234,9 +248,11 @@ __global__ void __launch_bounds__(kAT) __attribute__((amdgpu_waves_per_eu(4, 8))
       }
     }
   }
-  // block_sum's first barrier orders the scratch writes after the last reads of the block
+  }  // columns
+  // block_sum's first barrier orders the scratch writes after the last reads of
+  // the block; one partial per column slot (pass B sums all kAL3 of them)
   const double tot = block_sum<kAT>(static_cast<double>(fsum), reinterpret_cast<double*>(data));
-  if (tid == 0) a.partials[static_cast<size_t>(b) * gridDim.x + blockIdx.x] = tot;
+  if (tid < kNC) a.partials[static_cast<size_t>(b) * kAL3 + kNC * blockIdx.x + tid] = tid == 0 ? tot : 0.0;
 }
 
 }  // namespace
@@ -286,7 +302,7 @@ bool two_pass_supported(const FFTPlan3& plan, uint32_t n_unpadded) {
 
 hipError_t launch_pass_a(const FFTPlan3& plan, const PassAArgs& a, int batch, hipStream_t s) {
   if (!two_pass_supported(plan, a.n_unpadded)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(pass_a_kernel, dim3(kAL3, batch), dim3(kAT), 0, s, a);
+  hipLaunchKernelGGL(pass_a_kernel, dim3(kAL3 / kNC, batch), dim3(kAT), 0, s, a);
   return hipGetLastError();
 }
 
