@@ -557,6 +557,163 @@ __global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_
   }
 }
 
+// Composite radix R = A * B in registers (Cooley-Tukey, n = B n1 + n2,
+// k = k1 + A k2), twiddles W_R^e from tw(e); radices with a Dft<> run it.
+template <int R>
+struct RadixKind {
+  static constexpr bool kDirect = R == 2 || R == 3 || R == 4 || R == 5 || R == 8 || R == 16;
+};
+template <int R>
+struct RadixSplit;  // R = A * B with A a direct radix
+template <> struct RadixSplit<6> { static constexpr int A = 2, B = 3; };
+template <> struct RadixSplit<9> { static constexpr int A = 3, B = 3; };
+template <> struct RadixSplit<10> { static constexpr int A = 2, B = 5; };
+template <> struct RadixSplit<12> { static constexpr int A = 3, B = 4; };
+template <> struct RadixSplit<15> { static constexpr int A = 3, B = 5; };
+template <> struct RadixSplit<18> { static constexpr int A = 2, B = 9; };
+template <> struct RadixSplit<20> { static constexpr int A = 4, B = 5; };
+
+template <int R, class TW>
+__device__ __forceinline__ void dft_any(float2* v, TW tw) {
+  if constexpr (RadixKind<R>::kDirect) {
+    Dft<R>::run(v);
+  } else {
+    constexpr int A = RadixSplit<R>::A, B = RadixSplit<R>::B;
+    float2 y[A][B];
+#pragma unroll
+    for (int n2 = 0; n2 < B; ++n2) {
+      float2 t[A];
+#pragma unroll
+      for (int n1 = 0; n1 < A; ++n1) t[n1] = v[B * n1 + n2];
+      Dft<A>::run(t);
+#pragma unroll
+      for (int k1 = 0; k1 < A; ++k1) y[k1][n2] = (k1 * n2 == 0) ? t[k1] : cmul(t[k1], tw(k1 * n2));
+    }
+    // W_B^e = W_R^{A e}
+    auto twb = [&](int e) { return tw(A * e); };
+#pragma unroll
+    for (int k1 = 0; k1 < A; ++k1) {
+      float2 t[B];
+#pragma unroll
+      for (int n2 = 0; n2 < B; ++n2) t[n2] = y[k1][n2];
+      dft_any<B>(t, twb);
+#pragma unroll
+      for (int k2 = 0; k2 < B; ++k2) v[k1 + A * k2] = t[k2];
+    }
+  }
+}
+
+// Register-staged pass 2 for L = 16 * R1 with R1 not a divisor of 16 (96, 144,
+// 160, 192, 240, 288, 320: the chirp-z plans' lengths), two Stockham stages in
+// the other order than pass2r_kernel: radix 16 first (butterfly tj of a column
+// reads rows tj + R1 q, exactly the rows the thread loaded), then radix R1
+// (Ns = 16, butterflies j < 16 read rows j + 16 q and produce the natural-order
+// rows k2 = j + 16 q they store). The tile crosses LDS once; the generic
+// LDS-staged kernel crossed it once per stage (measured 22.3 us per million
+// elements at L2 = 288 against 5.4 for pass2r, profiles/kernel_stats_r4.txt).
+template <int L>
+__global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_per_eu(2, 8))) pass2g_kernel(Pass2Args a, uint32_t ntiles) {
+  constexpr int R1 = L / 16;
+  constexpr int TPC = R1;
+  constexpr int NT = kNcol * TPC;
+  constexpr int NB2 = (16 + TPC - 1) / TPC;  // stage-2 butterflies per thread (16 per column)
+  static_assert(L % 16 == 0 && 16 % R1 != 0, "L = 16 R1, R1 not a divisor of 16 (pass2r_kernel)");
+  constexpr int kLo = 1 << kP2LoBits;
+  __shared__ __attribute__((aligned(16))) float2 data[L * kNcol];
+  __shared__ float2 wl[L];  // W_L^e
+  __shared__ double red[NT / kWave + 1];
+  const float2* lo = a.tb.p2lo;
+  const float2* hi = a.tb.p2hi;
+
+  const uint32_t nblk3 = a.L3 / kNcol;
+  const uint32_t per_b = a.L1 * nblk3;
+  const size_t M = static_cast<size_t>(a.L1) * a.L2L3;
+  const int c = threadIdx.x % kNcol;
+  const int tj = threadIdx.x / kNcol;
+  auto tile_base = [&](uint32_t tl) -> const float2* {
+    const uint32_t b = tl / per_b, rem = tl % per_b;
+    const size_t off = static_cast<size_t>(b) * M + static_cast<size_t>(rem / nblk3) * a.L2L3 + (rem % nblk3) * kNcol;
+    const uint32_t lo32 = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(off));
+    const uint32_t hi32 = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(off >> 32));
+    return a.buf + ((static_cast<size_t>(hi32) << 32) | lo32);
+  };
+  auto col = [](int r, int cc) { return r * kNcol + cc; };
+  // loads: rows tj + R1 q = (lane offset of row tj) + q * (uniform R1 rows);
+  // stores: rows j + 16 q = (lane offset of row j) + q * (uniform 16 rows):
+  // one VGPR per access pattern, the row steps stay scalar
+  const uint32_t ld_off = (static_cast<uint32_t>(tj) * a.L3 + c) * sizeof(float2);
+  const size_t ld_step = static_cast<size_t>(R1) * a.L3;
+  const size_t st_step = static_cast<size_t>(16) * a.L3;
+  auto ld_at = [&](const float2* origin, int q) -> const float2* {
+    return reinterpret_cast<const float2*>(reinterpret_cast<const char*>(origin + q * ld_step) + ld_off);
+  };
+  // W_{R1}^e = W_L^{16 e}
+  auto tw1 = [&](int e) { return wl[(16 * e) % L]; };
+
+  float2 pre[16];
+  uint32_t tile = blockIdx.x;
+  if (tile < ntiles) {
+    const float2* src = tile_base(tile);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) pre[q] = *ld_at(src, q);
+  }
+  for (int e = threadIdx.x; e < L; e += NT) wl[e] = a.tb.st2[e + (e >> 4)];
+  __syncthreads();
+  while (tile < ntiles) {
+    const uint32_t b = __builtin_amdgcn_readfirstlane(tile / per_b);
+    const uint32_t rem = __builtin_amdgcn_readfirstlane(tile % per_b);
+    const uint32_t k1 = __builtin_amdgcn_readfirstlane(rem / nblk3);
+    const uint32_t n3 = (rem % nblk3) * kNcol + c;
+    float2* base = const_cast<float2*>(tile_base(tile));
+    const float2 wc = a.tb.p2col[k1 * a.L3 + n3];
+    // stage 1 (radix 16, Ns = 1): butterfly tj, outputs rows 16 tj + q
+    Dft<16>::run(pre);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) data[col(16 * tj + q, c)] = pre[q];
+    const uint32_t next = tile + gridDim.x;
+    if (next < ntiles) {  // in flight during the exchange, stage 2 and the stores
+      const float2* src = tile_base(next);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) pre[q] = *ld_at(src, q);
+    }
+    __syncthreads();
+    // stage 2 (radix R1, Ns = 16): butterfly j reads rows j + 16 q, twiddle W_L^{j q}
+    float2 y[NB2][R1];
+#pragma unroll
+    for (int v = 0; v < NB2; ++v) {
+      const int j = tj + TPC * v;
+      if (j < 16) {
+#pragma unroll
+        for (int q = 0; q < R1; ++q) y[v][q] = data[col(j + 16 * q, c)];
+#pragma unroll
+        for (int q = 1; q < R1; ++q) y[v][q] = cmul(y[v][q], wl[(j * q) % L]);
+        dft_any<R1>(y[v], tw1);
+      }
+    }
+    __syncthreads();  // LDS tile free for the next tile's stage 1
+    // outputs k2 = j + 16 q with W_M^{n3 (k1 + L1 k2)} = wc * W_{L2L3}^{n3 k2},
+    // exact every 8 rows and stepped by W_{L2L3}^{16 n3} in between
+    auto wexact = [&](uint32_t e) { return cmul(hi[e >> kP2LoBits], lo[e & (kLo - 1)]); };
+    const float2 step = wexact(n3 * 16u);
+#pragma unroll
+    for (int v = 0; v < NB2; ++v) {
+      const int j = tj + TPC * v;
+      if (j < 16) {
+        const uint32_t st_off = (static_cast<uint32_t>(j) * a.L3 + c) * sizeof(float2);
+        float2 t = make_float2(1.f, 0.f);
+#pragma unroll
+        for (int q = 0; q < R1; ++q) {
+          if (q % 8 == 0) t = cmul(wc, wexact(n3 * static_cast<uint32_t>(j + 16 * q)));
+          *reinterpret_cast<float2*>(reinterpret_cast<char*>(base + q * st_step) + st_off) = cmul(y[v][q], t);
+          t = cmul(t, step);
+        }
+      }
+    }
+    if (a.partials != nullptr && rem == 0) reduce_delta<NT>(a, b, red);
+    tile = next;
+  }
+}
+
 // ------------------------------------------------------------------ pass 3
 __device__ __forceinline__ size_t row_base(uint32_t c, uint32_t L1, uint32_t L2, uint32_t L3) {
   const uint32_t k1 = c % L1, k2 = c / L1;
@@ -980,6 +1137,22 @@ hipError_t launch_pass2(const FFTPlan3& plan, const Pass2Args& a, int batch, hip
     X(32) X(64) X(128) X(256)
 #undef X
     default: break;
+  }
+  // register-staged, radix 16 then R1 (L2 = 16 R1, R1 not a divisor of 16);
+  // BRP_P2G=0 (build switch): the LDS-staged kernel
+#ifndef BRP_P2G
+#define BRP_P2G 1
+#endif
+  if (BRP_P2G) {
+    switch (plan.L2) {
+#define X(n)                                                                                 \
+  case n:                                                                                    \
+    hipLaunchKernelGGL((pass2g_kernel<n>), grid, dim3(kNcol * (n / 16)), 0, s, a, ntiles);     \
+    return hipGetLastError();
+      X(96) X(144) X(160) X(192) X(240) X(288) X(320)
+#undef X
+      default: break;
+    }
   }
   switch (plan.L2) {
 #define X(n)                                                                \
