@@ -714,6 +714,70 @@ __global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_
   }
 }
 
+// Register-staged pass 1 for complex input (P1_COMPLEX / P1_COMPLEX_CONJ: the
+// chirp-z convolution transforms), L1 = 16 R1: the pass2g_kernel order --
+// radix 16 on the rows a thread loads (tj + R1 q), one LDS crossing, radix R1
+// producing the natural-order rows k1 = j + 16 q it stores with the output
+// twiddle W_{L1 L2}^{n2 k1}. The LDS-staged pass1_kernel crosses LDS once per
+// stage and bounds the chirp-z transforms (profiles/README.md, round 4).
+template <int L, int MODE>
+__global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_per_eu(2, 8))) pass1g_kernel(Pass1Args a) {
+  constexpr int R1 = L / 16;
+  constexpr int TPC = R1;
+  constexpr int NB2 = (16 + TPC - 1) / TPC;  // stage-2 butterflies per thread (16 per column)
+  static_assert(MODE == P1_COMPLEX || MODE == P1_COMPLEX_CONJ, "complex-input modes");
+  __shared__ __attribute__((aligned(16))) float2 data[L * kNcol];
+  __shared__ float2 wl[L];  // W_L^e
+
+  const int b = blockIdx.y;
+  const uint32_t nblk3 = a.L3 / kNcol;
+  const uint32_t n2 = blockIdx.x / nblk3;
+  const uint32_t col_base = n2 * a.L3 + (blockIdx.x % nblk3) * kNcol;
+  const size_t M = static_cast<size_t>(L) * a.L2L3;
+  const int c = threadIdx.x % kNcol;
+  const int tj = threadIdx.x / kNcol;
+  auto col = [](int r, int cc) { return r * kNcol + cc; };
+  auto tw1 = [&](int e) { return wl[(16 * e) % L]; };  // W_{R1}^e = W_L^{16 e}
+  if (a.reset != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *a.reset = 0;
+
+  // rows tj + R1 q: uniform row step R1 L2L3, one lane offset
+  const float2* src = a.cplx_in + static_cast<size_t>(b) * M + col_base + c + static_cast<size_t>(tj) * a.L2L3;
+  const size_t ld_step = static_cast<size_t>(R1) * a.L2L3;
+  float2 x[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const float2 v = src[q * ld_step];
+    x[q] = MODE == P1_COMPLEX_CONJ ? conjf2(v) : v;
+  }
+  for (int e = threadIdx.x; e < L; e += kNcol * TPC) wl[e] = a.tb.st1[e + (e >> 4)];
+  // stage 1 (radix 16, Ns = 1): butterfly tj, outputs rows 16 tj + q
+  Dft<16>::run(x);
+#pragma unroll
+  for (int q = 0; q < 16; ++q) data[col(16 * tj + q, c)] = x[q];
+  __syncthreads();
+  // stage 2 (radix R1, Ns = 16): butterfly j reads rows j + 16 q, twiddle W_L^{j q};
+  // outputs k1 = j + 16 q with W_{L1 L2}^{n2 k1} (p1 table)
+  float2* out = a.out + static_cast<size_t>(b) * M + col_base + c;
+  const float2* two = a.tb.p1 + static_cast<size_t>(n2) * L;
+#pragma unroll
+  for (int v = 0; v < NB2; ++v) {
+    const int j = tj + TPC * v;
+    if (j < 16) {
+      float2 y[R1];
+#pragma unroll
+      for (int q = 0; q < R1; ++q) y[q] = data[col(j + 16 * q, c)];
+#pragma unroll
+      for (int q = 1; q < R1; ++q) y[q] = cmul(y[q], wl[(j * q) % L]);
+      dft_any<R1>(y, tw1);
+#pragma unroll
+      for (int q = 0; q < R1; ++q) {
+        const int k1 = j + 16 * q;
+        out[static_cast<size_t>(k1) * a.L2L3] = cmul(y[q], two[k1]);
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------------ pass 3
 __device__ __forceinline__ size_t row_base(uint32_t c, uint32_t L1, uint32_t L2, uint32_t L3) {
   const uint32_t k1 = c % L1, k2 = c / L1;
@@ -1103,6 +1167,21 @@ hipError_t launch_pass1(const FFTPlan3& plan, Pass1Mode mode, const Pass1Args& a
   if (pad3 && plan.L1 == 96) {
     hipLaunchKernelGGL((pass1_pruned3_kernel<2>), grid, dim3(kNcol * 16), 0, s, a);
     return hipGetLastError();
+  }
+#ifndef BRP_P1G
+#define BRP_P1G 1  // register-staged complex-input pass 1 (build switch)
+#endif
+  if (BRP_P1G && (mode == P1_COMPLEX || mode == P1_COMPLEX_CONJ)) {
+    switch (plan.L1) {
+#define X(n)                                                                                         \
+  case n:                                                                                            \
+    if (mode == P1_COMPLEX) hipLaunchKernelGGL((pass1g_kernel<n, P1_COMPLEX>), grid, dim3(kNcol * (n / 16)), 0, s, a); \
+    else hipLaunchKernelGGL((pass1g_kernel<n, P1_COMPLEX_CONJ>), grid, dim3(kNcol * (n / 16)), 0, s, a);               \
+    return hipGetLastError();
+      X(96) X(144) X(160) X(192) X(240) X(288) X(320)
+#undef X
+      default: break;
+    }
   }
   switch (plan.L1) {
 #define X(n)                                                                                          \
