@@ -714,8 +714,9 @@ __global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_
   }
 }
 
-// Register-staged pass 1 for complex input (P1_COMPLEX / P1_COMPLEX_CONJ: the
-// chirp-z convolution transforms), L1 = 16 R1: the pass2g_kernel order --
+// Register-staged pass 1 for the chirp-z transforms (complex input:
+// P1_COMPLEX / P1_COMPLEX_CONJ; the chirp-multiplied resampled series:
+// P1_CHIRP2 / P1_CHIRP1 / P1_CHIRP1_PAIR, zero from Mb on), L1 = 16 R1: the pass2g_kernel order --
 // radix 16 on the rows a thread loads (tj + R1 q), one LDS crossing, radix R1
 // producing the natural-order rows k1 = j + 16 q it stores with the output
 // twiddle W_{L1 L2}^{n2 k1}. The LDS-staged pass1_kernel crosses LDS once per
@@ -725,9 +726,13 @@ __global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_
   constexpr int R1 = L / 16;
   constexpr int TPC = R1;
   constexpr int NB2 = (16 + TPC - 1) / TPC;  // stage-2 butterflies per thread (16 per column)
-  static_assert(MODE == P1_COMPLEX || MODE == P1_COMPLEX_CONJ, "complex-input modes");
+  constexpr bool kChirp = MODE == P1_CHIRP2 || MODE == P1_CHIRP1 || MODE == P1_CHIRP1_PAIR;
+  static_assert(kChirp || MODE == P1_COMPLEX || MODE == P1_COMPLEX_CONJ, "chirp-z modes");
+  constexpr int NT = kNcol * TPC;
   __shared__ __attribute__((aligned(16))) float2 data[L * kNcol];
   __shared__ float2 wl[L];  // W_L^e
+  __shared__ float lut_s[kLutSize], lut_c[kLutSize];
+  __shared__ double red[NT / kWave + 1];
 
   const int b = blockIdx.y;
   const uint32_t nblk3 = a.L3 / kNcol;
@@ -740,16 +745,64 @@ __global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_
   auto tw1 = [&](int e) { return wl[(16 * e) % L]; };  // W_{R1}^e = W_L^{16 e}
   if (a.reset != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *a.reset = 0;
 
-  // rows tj + R1 q: uniform row step R1 L2L3, one lane offset
-  const float2* src = a.cplx_in + static_cast<size_t>(b) * M + col_base + c + static_cast<size_t>(tj) * a.L2L3;
-  const size_t ld_step = static_cast<size_t>(R1) * a.L2L3;
   float2 x[16];
+  double sum = 0.0, sum_b = 0.0;  // sum_b: the second template of a pair (P1_CHIRP1_PAIR)
+  if constexpr (!kChirp) {
+    // rows tj + R1 q: uniform row step R1 L2L3, one lane offset
+    const float2* src = a.cplx_in + static_cast<size_t>(b) * M + col_base + c + static_cast<size_t>(tj) * a.L2L3;
+    const size_t ld_step = static_cast<size_t>(R1) * a.L2L3;
 #pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    const float2 v = src[q * ld_step];
-    x[q] = MODE == P1_COMPLEX_CONJ ? conjf2(v) : v;
+    for (int q = 0; q < 16; ++q) {
+      const float2 v = src[q * ld_step];
+      x[q] = MODE == P1_COMPLEX_CONJ ? conjf2(v) : v;
+    }
+  } else {
+    // the resampled series times the chirp W_{2Mb}^{n^2}, zero from Mb on
+    // (same arithmetic as pass1_kernel's chirp modes)
+    for (int i = threadIdx.x; i < kLutSize; i += NT) {
+      lut_s[i] = kSinLut[i];
+      lut_c[i] = kCosLut[i];
+    }
+    __syncthreads();
+    constexpr bool kPair = MODE == P1_CHIRP1_PAIR;
+    const bool fast = a.n_unpadded <= (1u << 23);
+    const int ta = kPair ? 2 * b : b;
+    const bool has_b = kPair && static_cast<uint32_t>(ta + 1) < a.n_tmpl;
+    const TemplateDev td = a.tmpl[ta];
+    TemplateDev tdb = td;
+    if (has_b) tdb = a.tmpl[ta + 1];
+    const float* series = a.series + static_cast<size_t>(td.wu) * a.n_unpadded;
+    const float* series_b = a.series + static_cast<size_t>(tdb.wu) * a.n_unpadded;
+    const int last = static_cast<int>(a.n_unpadded) - 1;
+    auto sample_of = [&](const TemplateDev& t, const float* ser, uint32_t m) -> float {
+      if (m >= t.n_steps) return 0.0f;
+      const float dt = resamp_del_t(m, t.p, lut_s, lut_c);
+      const int i = min(max(fast ? resamp_nearest_f(m, dt) : resamp_nearest(m, dt), 0), last);
+      return ser[i] - t.mu0;
+    };
+    float fsum = 0.0f, fsum_b = 0.0f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const uint32_t n = static_cast<uint32_t>(tj + R1 * q) * a.L2L3 + col_base + c;
+      float2 v = make_float2(0.0f, 0.0f);
+      if (n < a.Mb) {
+        float2 xs;
+        if (MODE == P1_CHIRP2) {
+          xs = make_float2(sample_of(td, series, 2 * n), sample_of(td, series, 2 * n + 1));
+          fsum += xs.x + xs.y;
+        } else {
+          xs = make_float2(sample_of(td, series, n), has_b ? sample_of(tdb, series_b, n) : 0.0f);
+          fsum += xs.x;
+          fsum_b += xs.y;
+        }
+        v = cmul(xs, tw_lookup(a.chirp, static_cast<uint64_t>(n) * n));  // W_{2Mb}^{n^2 mod 2Mb}
+      }
+      x[q] = v;
+    }
+    sum = static_cast<double>(fsum);
+    sum_b = static_cast<double>(fsum_b);
   }
-  for (int e = threadIdx.x; e < L; e += kNcol * TPC) wl[e] = a.tb.st1[e + (e >> 4)];
+  for (int e = threadIdx.x; e < L; e += NT) wl[e] = a.tb.st1[e + (e >> 4)];
   // stage 1 (radix 16, Ns = 1): butterfly tj, outputs rows 16 tj + q
   Dft<16>::run(x);
 #pragma unroll
@@ -774,6 +827,18 @@ __global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_
         const int k1 = j + 16 * q;
         out[static_cast<size_t>(k1) * a.L2L3] = cmul(y[q], two[k1]);
       }
+    }
+  }
+  if constexpr (MODE == P1_CHIRP2 || MODE == P1_CHIRP1) {
+    const double tot = block_sum<NT>(sum, red);
+    if (threadIdx.x == 0) a.partials[static_cast<size_t>(b) * gridDim.x + blockIdx.x] = tot;
+  } else if constexpr (MODE == P1_CHIRP1_PAIR) {  // partial sums per template (2b, 2b + 1)
+    const double tot = block_sum<NT>(sum, red);
+    const double tot_b = block_sum<NT>(sum_b, red);
+    if (threadIdx.x == 0) {
+      a.partials[static_cast<size_t>(2 * b) * gridDim.x + blockIdx.x] = tot;
+      if (static_cast<uint32_t>(2 * b + 1) < a.n_tmpl)
+        a.partials[static_cast<size_t>(2 * b + 1) * gridDim.x + blockIdx.x] = tot_b;
     }
   }
 }
@@ -1171,13 +1236,18 @@ hipError_t launch_pass1(const FFTPlan3& plan, Pass1Mode mode, const Pass1Args& a
 #ifndef BRP_P1G
 #define BRP_P1G 1  // register-staged complex-input pass 1 (build switch)
 #endif
-  if (BRP_P1G && (mode == P1_COMPLEX || mode == P1_COMPLEX_CONJ)) {
+  if (BRP_P1G && mode != P1_RESAMPLE && mode != P1_REAL) {
     switch (plan.L1) {
 #define X(n)                                                                                         \
-  case n:                                                                                            \
-    if (mode == P1_COMPLEX) hipLaunchKernelGGL((pass1g_kernel<n, P1_COMPLEX>), grid, dim3(kNcol * (n / 16)), 0, s, a); \
-    else hipLaunchKernelGGL((pass1g_kernel<n, P1_COMPLEX_CONJ>), grid, dim3(kNcol * (n / 16)), 0, s, a);               \
-    return hipGetLastError();
+  case n: {                                                                                          \
+    const dim3 blk(kNcol * (n / 16));                                                                \
+    if (mode == P1_COMPLEX) hipLaunchKernelGGL((pass1g_kernel<n, P1_COMPLEX>), grid, blk, 0, s, a);  \
+    else if (mode == P1_COMPLEX_CONJ) hipLaunchKernelGGL((pass1g_kernel<n, P1_COMPLEX_CONJ>), grid, blk, 0, s, a); \
+    else if (mode == P1_CHIRP2) hipLaunchKernelGGL((pass1g_kernel<n, P1_CHIRP2>), grid, blk, 0, s, a);             \
+    else if (mode == P1_CHIRP1) hipLaunchKernelGGL((pass1g_kernel<n, P1_CHIRP1>), grid, blk, 0, s, a);             \
+    else hipLaunchKernelGGL((pass1g_kernel<n, P1_CHIRP1_PAIR>), grid, blk, 0, s, a);                               \
+    return hipGetLastError();                                                                        \
+  }
       X(96) X(144) X(160) X(192) X(240) X(288) X(320)
 #undef X
       default: break;
