@@ -1,7 +1,9 @@
 """Two ranks over RCCL on two MI355X devices (pytest -m gpu; skipped on a
 one-GPU box): the sharded search with the all-gathered, rank-ordered merge
 equals the one-process table byte for byte, and the chunked search seeds each
-rank with the global floors (parallel/dist.py)."""
+rank with the global floors (parallel/dist.py). On a one-GPU box two ranks
+share device 0 over gloo instead: the same multi-process path (GPU engines in
+two processes, floor exchange during the step, all-gather, merge) without RCCL."""
 import os
 import socket
 
@@ -20,14 +22,15 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, opts, out_dir):
-    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
-                      MASTER_PORT=str(port))
+def _worker(rank, world, port, opts, out_dir, backend="nccl"):
+    # gloo: the ranks share device 0 (LOCAL_RANK 0 selects the engines' GPU)
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank if backend == "nccl" else 0),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch.distributed as dist
 
-    ctx = pdist.init_distributed("nccl")  # RCCL; the device is set per LOCAL_RANK first
+    ctx = pdist.init_distributed(backend)  # RCCL: the device is set per LOCAL_RANK first
     try:
-        assert ctx.backend == "nccl"
+        assert ctx.backend == backend
         ss = pdist.ShardedSearch(opts, ctx, streams=2)
         table = ss.step()
         chunked, n = ss.search(chunk=9)
@@ -71,6 +74,24 @@ def test_rccl_two_ranks_equal_single(brp, gpu, tmp_path):
     opts = dict(inputfile=case["wu"], templatebank=case["bank"], zaplistfile=case["zap"], f0=400.0, padding=3.0,
                 fA=0.08, window=100, white=True, batch=2)
     mp.start_processes(_worker, args=(2, _free_port(), opts, str(tmp_path)), nprocs=2, join=True,
+                       start_method="spawn")
+    merged = np.load(tmp_path / "merged.npy")
+    r = brp.run_search(dict(opts), 0, 0, False, False)
+    assert r["templates_run"] == 30
+    assert bytes(np.asarray(r["table"].to_bytes(), np.uint8)) == bytes(merged)
+
+
+def test_two_ranks_sharing_one_gpu_gloo(brp, gpu, tmp_path):
+    """Two rank processes on device 0 over gloo: GPU engines in each process,
+    the level floors exchanged during the step, the all-gathered rank-ordered
+    merge equal to the one-process table byte for byte."""
+    import torch.multiprocessing as mp
+
+    inj = synth.Injection(f0=173.0, P_orb=1200.0, tau=0.05, psi0=2.0, amplitude=3.0)
+    case = synth.synthetic_case(tmp_path / "case", n=1 << 16, n_templates=29, inj=inj)
+    opts = dict(inputfile=case["wu"], templatebank=case["bank"], zaplistfile=case["zap"], f0=400.0, padding=3.0,
+                fA=0.08, window=100, white=True, batch=2)
+    mp.start_processes(_worker, args=(2, _free_port(), opts, str(tmp_path), "gloo"), nprocs=2, join=True,
                        start_method="spawn")
     merged = np.load(tmp_path / "merged.npy")
     r = brp.run_search(dict(opts), 0, 0, False, False)
