@@ -179,3 +179,38 @@ def test_odd_length_template_pairs_match_single(brp, gpu, tmp_path, monkeypatch)
         _compare_tables(pair.table, single.table, rtol=1e-5)
         c = BRPSearch(SearchConfig(use_cpu=True, **cfg), gpus=8).run(write_output=False, use_checkpoint=False)
         _compare_tables(pair.table, c.table)
+
+
+# (samples, padding) whose chirp-z plans put every length of the
+# register-staged passes (fft_passes.hip pass1g_kernel for L1, pass2g_kernel
+# for L2: 96, 144, 160, 192, 240, 288, 320) in place at least once
+# (found with derive_geometry + brp.bluestein_plan; the plan is asserted below)
+_REG_CASES = [
+    (1 << 16, 5.01, (144, 48)), (1 << 16, 6.26, (96, 48)), (1 << 17, 7.51, (144, 144)), (1 << 17, 8.46, (96, 96)),
+    (1 << 18, 5.63, (240, 80)), (1 << 18, 6.02, (160, 80)), (1 << 19, 5.87, (192, 128)), (1 << 19, 6.01, (160, 160)),
+    (1 << 19, 7.51, (288, 144)), (1 << 19, 8.44, (240, 240)), (1 << 19, 8.8, (192, 192)), (1 << 20, 6.04, (320, 160)),
+    (1 << 20, 7.54, (288, 288)), (1 << 21, 6.02, (320, 320)),
+]
+
+
+@pytest.mark.parametrize("n,padding,l12", _REG_CASES)
+def test_register_staged_pass_lengths(brp, gpu, tmp_path, monkeypatch, n, padding, l12):
+    """Every L1 / L2 of the register-staged chirp-z passes: the device
+    spectrum of one template against the CPU double-precision spectrum (the
+    CPU model pads with the accurate mean, as the device does: at 2^21 samples
+    the reference CPU build's serial float mean moves the lowest bins)."""
+    monkeypatch.setenv("BRP_CPU_MEAN", "double")
+    _, series, geom = _geom(brp, tmp_path, n, padding)
+    N = geom["nsamples"]
+    plan = brp.bluestein_plan(N if N % 2 else N // 2)
+    assert plan is not None and (plan[1], plan[2]) == l12, (N, plan)
+    eng = brp.HipEngine()
+    eng.init(0, 2)
+    eng.setup(geom, series, float(np.mean(series)))
+    ps_g, ns_g = eng.power_spectrum(900.0, 0.05, 1.3)
+    xr, ns_c, _ = brp.cpu_resample(series, geom, 900.0, 0.05, 1.3)
+    ps_c = brp.cpu_power_spectrum(xr, geom["fft_size"])
+    assert ns_g == ns_c
+    scale = float(np.mean(ps_c[1:]))
+    err = np.abs(ps_g.astype(np.float64) - ps_c)[1:] / np.maximum(ps_c[1:], scale)
+    assert err.max() < 2e-4, (N, padding, l12, err.max(), int(np.argmax(err)) + 1)
