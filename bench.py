@@ -18,6 +18,7 @@ per step is fixed, `value` is templates/s of the whole job.
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -123,22 +124,78 @@ def recall_vs_golden(table, geom) -> dict | None:
     return rec
 
 
+def visible_gpus(topology: str = "/sys/class/kfd/kfd/topology/nodes", dev_dir: str = "/dev/dri") -> int:
+    """GPUs this process may use, counted without any HIP call (so the bench
+    parent never creates a HIP context its rank processes could inherit, and
+    never depends on whether torch.cuda.device_count() falls back to
+    hipGetDeviceCount): KFD topology nodes with a non-zero gfx_target_version
+    whose DRM render node is present and accessible, then narrowed by
+    ROCR_VISIBLE_DEVICES and HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES in the
+    runtime's order (each list indexes the devices the previous one left; the
+    list ends at its first invalid entry; an empty list hides every device)."""
+    try:
+        nodes = sorted(os.listdir(topology), key=lambda x: int(x) if x.isdigit() else 1 << 30)
+    except OSError:
+        return 0
+    n = 0
+    for node in nodes:
+        try:
+            with open(os.path.join(topology, node, "properties")) as fh:
+                props = dict(ln.split(None, 1) for ln in fh.read().splitlines() if len(ln.split(None, 1)) == 2)
+        except (OSError, ValueError):
+            continue
+        try:
+            if int(props.get("gfx_target_version", "0")) == 0:
+                continue  # a CPU node
+            minor = int(props.get("drm_render_minor", "-1"))
+        except ValueError:
+            continue
+        render = os.path.join(dev_dir, f"renderD{minor}")
+        if minor >= 0 and os.path.exists(render) and not os.access(render, os.R_OK | os.W_OK):
+            continue  # present in the topology, not ours (device cgroup / permissions)
+        n += 1
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        val = os.environ.get(var)
+        if val is None:
+            continue
+        if var == "CUDA_VISIBLE_DEVICES" and os.environ.get("HIP_VISIBLE_DEVICES") is not None:
+            continue  # HIP's own variable wins
+        kept, seen = 0, set()
+        for tok in (t.strip() for t in val.split(",")):
+            if not tok:
+                break
+            if tok.isdigit():
+                if int(tok) >= n or tok in seen:
+                    break
+                seen.add(tok)
+            kept += 1  # a UUID (ROCR) names one device
+        n = min(n, kept)
+    return n
+
+
+def share_device() -> bool:
+    """BRP_BENCH_SHARE_DEVICE=1 (tests only): every rank runs on device 0 and
+    the ranks talk over gloo, so the self-launched multi-rank path (rank
+    processes, floor exchange, all-gather, merge) runs on a one-GPU box. Not a
+    throughput measurement: the JSON line says so."""
+    return os.environ.get("BRP_BENCH_SHARE_DEVICE") == "1"
+
+
 def launch_ranks(args) -> int:
     """`--gpus N` (N > 1) without a launcher environment: start the N rank
     processes here, one per GPU, the way torch.distributed.run would
     (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT).
-    Nothing in this process touches the GPU (device_count does not initialise
-    HIP), so no rank inherits a HIP context. Rank 0 prints the JSON line.
-    Fewer visible devices than N is an error, never a silent 1-GPU run."""
+    Nothing in this process touches the GPU (the devices are counted from
+    sysfs, visible_gpus), so no rank inherits a HIP context. Rank 0 prints the
+    JSON line. Fewer visible devices than N is an error, never a silent 1-GPU
+    run (BRP_BENCH_SHARE_DEVICE=1: one device is enough, see share_device)."""
     import socket
     import subprocess
 
     n = args.gpus
     if not args.cpu:
-        import torch
-
-        have = torch.cuda.device_count()
-        if have < n:
+        have = visible_gpus()
+        if have < (1 if share_device() else n):
             print(f"[bench] error: --gpus {n} but only {have} HIP device(s) are visible", file=sys.stderr)
             return 2
     with socket.socket() as s:
@@ -182,10 +239,11 @@ def main() -> int:
     if not args.shard_of and world_env != args.gpus:
         print(f"[bench] error: --gpus {args.gpus} but WORLD_SIZE={world_env}", file=sys.stderr)
         return 2
-    if not args.cpu and not args.shard_of and torch.cuda.device_count() < world_env:
+    shared = share_device() and not args.cpu and world_env > 1
+    if not args.cpu and not args.shard_of and not shared and torch.cuda.device_count() < world_env:
         print(f"[bench] error: {world_env} ranks but only {torch.cuda.device_count()} HIP device(s)", file=sys.stderr)
         return 2
-    ctx = init_distributed("gloo" if args.cpu else None)
+    ctx = init_distributed("gloo" if (args.cpu or shared) else None)
     if args.shard_of:
         from boinc_app_eah_brp_amd.parallel import DistContext
 
@@ -225,7 +283,8 @@ def main() -> int:
         search = MultiWUSearch([str(wu)] + extra, cfg, pipelines=args.streams, ctx=ctx)
         data_desc += f" + {n_wus - 1} synthetic WUs of the same shape (noise + injected binary pulsars)"
     else:
-        search = ShardedSearch(opts, ctx, streams=1 if args.cpu else args.streams, use_cpu=args.cpu)
+        search = ShardedSearch(opts, ctx, device=0 if shared else None, streams=1 if args.cpu else args.streams,
+                               use_cpu=args.cpu)
     limit = args.templates if args.templates > 0 else search.total
 
     def first_table(t):
@@ -298,6 +357,7 @@ def main() -> int:
             "launched_by": "bench.py" if os.environ.get("BRP_BENCH_LAUNCHED") else
                            ("torch.distributed.run" if world > 1 else "single process"),
             "table_identical_to_warmup": (first == bytes(table.to_bytes())) if first is not None else None,
+            "table_sha256": hashlib.sha256(bytes(table.to_bytes())).hexdigest(),
             "busy_span_ms_rank0": round(stats["busy_span_ms"], 3),
             "device_candidates_per_template_rank0": round(stats.get("candidates", 0) / max(1, stats["templates"]), 2),
             "bounded_output_batches_rank0": stats.get("select_batches", 0),
@@ -315,6 +375,9 @@ def main() -> int:
                 "work_units": n_wus,
             },
         }
+        if shared:
+            out["shared_device"] = ("all ranks ran on device 0 over gloo (BRP_BENCH_SHARE_DEVICE=1): a test of the "
+                                    "multi-rank launch, not a multi-GPU throughput")
         if ctx.solo_shard:
             out["shard_of"] = {"world": ctx.world, "rank": ctx.rank, "templates": work,
                                "note": "compute-only timing of one rank's block on one GPU (no collectives)"}

@@ -36,7 +36,7 @@ HOST_SRCS = [
     "app/search.cpp", "app/multi.cpp", "app/passes.cpp", "app/cli.cpp",
 ]
 DEVICE_SRCS = [
-    "hip/fft_passes.hip", "hip/fft_two_pass.hip", "hip/bluestein.hip", "hip/harmonic_sum.hip", "hip/resample.hip", "hip/whiten.hip", "hip/rmed_wide.hip",
+    "hip/fft_passes.hip", "hip/bluestein.hip", "hip/harmonic_sum.hip", "hip/resample.hip", "hip/whiten.hip", "hip/rmed_wide.hip",
 ]
 BINDING_SRCS = ["bindings/pybind.cpp"]
 APP_MAIN = "app/main.cpp"

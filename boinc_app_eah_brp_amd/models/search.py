@@ -73,7 +73,7 @@ class BRPSearch:
                             timings=dict(setup=r["t_setup"], templates=r["t_templates"], total=r["t_total"],
                                          busy_span_ms=r["busy_span_ms"], whiten_ms=r["whiten_ms"]),
                             stats=dict(overflow_reruns=r["overflow_reruns"], select_batches=r["select_batches"],
-                                       select_exits=r["select_exits"]))
+                                       select_exits=r["select_exits"], tie_reruns=r["tie_reruns"]))
 
     def results(self):
         lines, done = self.brp.read_results(self.config.outputfile)

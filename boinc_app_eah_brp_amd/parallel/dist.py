@@ -363,6 +363,11 @@ class ShardedSearch:
                     raise RuntimeError(f"checkpoint {cp}: {n_cp} templates done > bank size {self.total}")
                 n, table = int(n_cp), t
         t0 = time.perf_counter()
+        # No FloorSync runs here (each chunk is seeded with the merged prefix
+        # table instead): floors a previous step() left behind must not prune
+        # this search, or a bin whose power equals one of them is dropped on
+        # its own rank and the level ends short of 100 entries.
+        self.session.reset_external_floors()
         self.session.prepare()
         t1 = time.perf_counter()
         search_s = 0.0

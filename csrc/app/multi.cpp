@@ -83,6 +83,7 @@ BackendStats MultiSession::stats() const {
     t.templates += s.templates;
     t.batches += s.batches;
     t.overflow_reruns += s.overflow_reruns;
+    t.tie_reruns += s.tie_reruns;
     t.select_batches += s.select_batches;
     t.select_exits += s.select_exits;
     t.list_dma_copies += s.list_dma_copies;

@@ -213,6 +213,7 @@ BackendStats SearchSession::stats() const {
     t.templates += s.templates;
     t.batches += s.batches;
     t.overflow_reruns += s.overflow_reruns;
+    t.tie_reruns += s.tie_reruns;
     t.select_batches += s.select_batches;
     t.select_exits += s.select_exits;
     t.list_dma_copies += s.list_dma_copies;
@@ -286,7 +287,7 @@ int SearchSession::open(const SearchOptions& opt, const SearchControl& ctl) {
   }
   if (!d.opt.use_cpu && !hip_backend_supports(d.g)) {
     // Every N the reference can form on a real work unit has a plan: the
-    // three-pass FFT for N/2 = L1*L2*L3 over 16*2^a*3^b*5^c lengths, the chirp-z
+    // three-pass FFT for N/2 = L1*L2*L3 over 16*2^a*3^b*5^c*7^d lengths, the chirp-z
     // transform over such a length for all others (convolution length < 2^31,
     // i.e. N < ~2^30). Beyond that the product path refuses loudly; it never
     // switches to the CPU golden model behind the user's back.
@@ -488,7 +489,15 @@ int SearchSession::run(uint32_t begin, uint32_t end, CandidateTable& table, Sear
           std::lock_guard<std::mutex> lk(mu);
           std::memcpy(thr, thr_shared, sizeof(thr));
         }
-        for (int h = 0; h < kNumHarmonicLevels; ++h) thr[h] = std::fmax(thr[h], d.ext(h));
+        // Other ranks' floors prune the device output: a bin below every
+        // merged-table floor can never enter it. The device emits p > thr, so
+        // the threshold is the float just below the external floor: a bin whose
+        // power equals it is still emitted, and the in-order tie rules
+        // (demod_binary.c:1345, strict >) decide it exactly as in the merge.
+        for (int h = 0; h < kNumHarmonicLevels; ++h) {
+          const float e = d.ext(h);
+          if (e > 0.0f) thr[h] = std::fmax(thr[h], std::nextafter(e, 0.0f));
+        }
         boinc::begin_critical_section();
         const int rc = be->submit(&d.tin[first], n, thr);
         if (rc) {

@@ -21,7 +21,6 @@
 #include "../core/rngmed.hpp"
 #include "../core/search_core.hpp"
 #include "../core/stats.hpp"
-#include "../hip/two_pass_check.hpp"
 #include "../core/wisdom.hpp"
 #include "../engine/hip_engine.hpp"
 
@@ -435,6 +434,10 @@ PYBIND11_MODULE(_brp, m) {
              WorkUnit wu;
              check(read_work_unit(path, wu), "read_work_unit");
              check(e.setup_packed(dict_to_geometry(gd), wu, mu0), "HipEngine.setup_packed");
+             // the payload upload is queued from `wu`, which dies with this
+             // scope: wait for it (the app pins and keeps its WU buffer instead)
+             if (hipSetDevice(e.device()) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+               throw std::runtime_error("HipEngine.setup_from_wu: device synchronisation failed");
            })
       .def("download_series",
            [](HipEngine& e) {
@@ -522,6 +525,7 @@ PYBIND11_MODULE(_brp, m) {
         d["templates"] = s.templates;
         d["batches"] = s.batches;
         d["overflow_reruns"] = s.overflow_reruns;
+        d["tie_reruns"] = s.tie_reruns;
         d["select_batches"] = s.select_batches;
         d["list_dma_copies"] = s.list_dma_copies;
         d["shared_series_batches"] = s.shared_series_batches;
@@ -533,8 +537,6 @@ PYBIND11_MODULE(_brp, m) {
     if (!make_fft_plan(M, p)) return py::none();
     return py::make_tuple(p.L1, p.L2, p.L3);
   });
-  m.def("two_pass_selftest", [] { return hipk::two_pass_selftest(); },
-        "host-side check of the two-pass plan's index algebra (\"\" = ok)");
   m.def("bluestein_plan", [](uint32_t Mb) -> py::object {
     FFTPlan3 p;
     if (!make_bluestein_plan(Mb, p)) return py::none();
@@ -575,6 +577,7 @@ PYBIND11_MODULE(_brp, m) {
         d["busy_span_ms"] = res.stats.busy_span_ms;
         d["whiten_ms"] = res.stats.whiten_ms;
         d["overflow_reruns"] = res.stats.overflow_reruns;
+        d["tie_reruns"] = res.stats.tie_reruns;
         d["select_batches"] = res.stats.select_batches;
         d["select_exits"] = res.stats.select_exits;
         return d;
@@ -639,6 +642,7 @@ PYBIND11_MODULE(_brp, m) {
         d["templates"] = st.templates;
         d["batches"] = st.batches;
         d["overflow_reruns"] = st.overflow_reruns;
+        d["tie_reruns"] = st.tie_reruns;
         d["select_batches"] = st.select_batches;
         d["select_exits"] = st.select_exits;
         d["list_dma_copies"] = st.list_dma_copies;
@@ -702,6 +706,7 @@ PYBIND11_MODULE(_brp, m) {
         d["batches"] = st.batches;
         d["candidates"] = st.candidates;
         d["overflow_reruns"] = st.overflow_reruns;
+        d["tie_reruns"] = st.tie_reruns;
         d["select_batches"] = st.select_batches;
         d["shared_series_batches"] = st.shared_series_batches;
         return d;

@@ -9,6 +9,8 @@
 //   hip_oom[:N]            every device allocation (after the first N) fails
 //                          (-> temporary exit)
 //   pinned_fail            every pinned host allocation fails (-> pageable)
+//   hs_cap_raw             BRP_HS_CAP is taken as is, below the bounded output's size
+//                          (the bounded output overflows: tie-storm re-run)
 //   segv_after_template:N  invalid store once N templates are done (crash report)
 //   slow_template:MS       sleep MS ms per applied template (paces client tests)
 //   resource_error         the search returns a host allocation failure

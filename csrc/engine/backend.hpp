@@ -34,6 +34,7 @@ struct BackendStats {
   uint64_t templates = 0;
   uint64_t batches = 0;
   uint64_t overflow_reruns = 0;   // batches re-run with the bounded output after a list overflow
+  uint64_t tie_reruns = 0;        // batches whose bounded output overflowed too (ties at a 100th place): re-run into a list sized to it
   uint64_t select_batches = 0;    // batches that ran with the bounded output
   uint64_t select_exits = 0;      // returns to the compacting path (floors rose)
   uint64_t list_dma_copies = 0;   // long candidate lists DMA-copied instead of read in place

@@ -45,12 +45,12 @@ using hipk::TemplateDev;
 namespace {
 constexpr uint64_t kMaxL2L3 = 256ull * 512;  // W_{L2 L3} as lo[256] x hi[512] (build_tables)
 const uint32_t kPlanP3[] = {256, 320, 192, 160, 128, 96, 64};
-const uint32_t kPlanP12[] = {512, 384, 320, 288, 256, 240, 192, 160, 144, 128, 96, 80, 64, 48, 32, 16};
+const uint32_t kPlanP12[] = {512, 448, 384, 320, 288, 256, 240, 224, 192, 160, 144, 128, 112, 96, 80, 64, 48, 32, 16};
 }  // namespace
 
 // Chirp-z transform of length Mb (bluestein_kernels.hpp): the smallest length
 // L >= 2 Mb - 1 the three-pass FFT factors. The products L1 L2 L3 of the
-// compiled lengths are dense (16 * 2^a 3^b 5^c), so L stays within ~10 % of
+// compiled lengths are dense (16 * 2^a 3^b 5^c 7^d), so L stays within ~10 % of
 // the minimum.
 bool make_bluestein_plan(uint32_t Mb, FFTPlan3& plan) {
   const uint64_t need = 2ull * Mb - 1;
@@ -252,7 +252,6 @@ std::vector<float2> stage_table_rows(uint32_t L) {
 // so they are computed once: ~80 000 long-double sin/cos per plan.
 struct HostTables {
   std::vector<float2> st1, st2, st3, p1, p2col, p2lo, p2hi, p3;
-  std::vector<float2> a1024, a48;  // two-pass plan: W_1024^e, W_48^e
 };
 
 const HostTables& host_tables(const FFTPlan3& plan) {
@@ -282,10 +281,6 @@ const HostTables& host_tables(const FFTPlan3& plan) {
   h->p3.assign(32 + 4ull * L3 / 32, make_float2(0, 0));
   for (uint32_t i = 0; i < 32; ++i) h->p3[i] = root(i, 4ull * L3);
   for (uint32_t m = 0; m < 4 * L3 / 32; ++m) h->p3[32 + m] = root(32ull * m, 4ull * L3);
-  h->a1024.resize(1024);
-  for (uint32_t e = 0; e < 1024; ++e) h->a1024[e] = root(e, 1024);
-  h->a48.resize(48);
-  for (uint32_t e = 0; e < 48; ++e) h->a48[e] = root(e, 48);
   slot = std::move(h);
   return *slot;
 }
@@ -409,6 +404,7 @@ struct HipEngine::Impl {
   int hs_cell_shift = 3;        // its bound cells: 8 bins (BRP_HS_CELL=4: 4 bins, tighter bounds but
                                 // 44 KB LDS / 125 VGPRs per workgroup: 16.4-16.7k vs 15.6-15.8k templates/s)
   bool hs_xcd = false;          // pruned HS: contiguous block ranges per XCD (BRP_HS_XCD=1)
+  bool lds_pass1 = false;       // resampling pass 1 on the LDS-staged kernel (BRP_P1_LDS=1, A/B)
   bool hs_direct = true;        // bounds read straight from global memory (BRP_HS_DIRECT=0: LDS-staged;
                                 // +2 % fp32, +3 % config 5 in one call, profiles/README.md round 3)
   DevBuf<double> partials;      // [batch][wg1]
@@ -485,13 +481,6 @@ struct HipEngine::Impl {
     w_pending = false;
   }
   DevBuf<float2> t_st1, t_st2, t_st3, t_p1, t_p2col, t_p2lo, t_p2hi, t_p3;
-  DevBuf<float2> t_a1024, t_a48;
-  DevBuf<float> t_lut;  // kSinLut | kCosLut (pass A reads the LUT through the caches)
-  // Two-pass plan for the benchmark geometry (fft_two_pass.hip): pass A = the
-  // resampling gather and the whole 24576-point column transform, pass B =
-  // pass 3 on transposed row tiles; 100 MB less memory traffic per template
-  // than the three passes. Opt-in (BRP_TWO_PASS=1) while it is slower.
-  bool two_pass = false;
 
   struct { TemplateDev* p = nullptr; } h_tmpl;
   struct { float* p = nullptr; } h_thr;
@@ -500,7 +489,7 @@ struct HipEngine::Impl {
   uint32_t slots = 1;           // work-unit slots of the series buffer (multi-WU batching)
   std::vector<float> mu0s;      // per-slot padding offset
 
-  std::map<int, hipGraphExec_t> graphs;  // key: batch size * kIoSlots + I/O slot
+  std::map<int, hipGraphExec_t> graphs;  // key: (batch size * kIoSlots + I/O slot) * 2 + select mode
   BackendStats st;
 
   hipk::FFTTables tables() const {
@@ -529,14 +518,8 @@ struct HipEngine::Impl {
     int rc;
     if ((rc = upload(t_st1, h.st1)) || (rc = upload(t_st2, h.st2)) || (rc = upload(t_st3, h.st3)) ||
         (rc = upload(t_p1, h.p1)) || (rc = upload(t_p2col, h.p2col)) || (rc = upload(t_p2lo, h.p2lo)) ||
-        (rc = upload(t_p2hi, h.p2hi)) || (rc = upload(t_p3, h.p3)) || (rc = upload(t_a1024, h.a1024)) ||
-        (rc = upload(t_a48, h.a48)))
+        (rc = upload(t_p2hi, h.p2hi)) || (rc = upload(t_p3, h.p3)))
       return rc;
-    std::vector<float> lut(kSinLut, kSinLut + kLutSize);
-    lut.insert(lut.end(), kCosLut, kCosLut + kLutSize);
-    if ((rc = t_lut.alloc(lut.size()))) return rc;
-    if (copy_sync(t_lut.p, lut.data(), lut.size() * sizeof(float), hipMemcpyHostToDevice, stream) != hipSuccess)
-      return RADPUL_HIP_MEM_COPY_HOST_DEVICE;
     return 0;
   }
 
@@ -694,25 +677,10 @@ struct HipEngine::Impl {
     if (stream) (void)hipStreamDestroy(stream);
   }
 
-  // Template transform up to the complex array: pass 1 (+ pass 2), or pass A
-  // of the two-pass plan. `reset`: the batch's candidate counter to zero.
+  // Template transform, pass 1 (fused resampling gather). `reset`: the
+  // batch's candidate counter to zero.
   hipError_t fft_pass1(int nb, uint32_t* reset) {
     const hipk::TwiddleTable tw = twt();
-    if (two_pass) {
-      hipk::PassAArgs aa{};
-      aa.out = buf.p;
-      aa.tw = tw;
-      aa.w1024 = t_a1024.p;
-      aa.w48 = t_a48.p;
-      aa.lut_sin = t_lut.p;
-      aa.lut_cos = t_lut.p + kLutSize;
-      aa.series = series_in();
-      aa.n_unpadded = g.n_unpadded;
-      aa.tmpl = tmpl.p;
-      aa.partials = partials.p;
-      aa.reset = reset;
-      return hipk::launch_pass_a(plan, aa, nb, stream);
-    }
     hipk::Pass1Args a1{};
     a1.out = buf.p;
     a1.L2L3 = plan.L2 * plan.L3;
@@ -724,10 +692,10 @@ struct HipEngine::Impl {
     a1.tmpl = tmpl.p;
     a1.partials = partials.p;
     a1.reset = reset;
+    a1.lds_pass1 = lds_pass1;
     return hipk::launch_pass1(plan, hipk::P1_RESAMPLE, a1, nb, stream);
   }
   hipError_t fft_pass2(int nb) {
-    if (two_pass) return hipSuccess;  // pass A did the whole column transform
     hipk::Pass2Args a2{};
     a2.buf = buf.p;
     a2.L1 = plan.L1;
@@ -759,9 +727,6 @@ struct HipEngine::Impl {
     a3.norm = static_cast<float>(1.0 / g.nsamples);
     a3.tmpl = tmpl.p;
     a3.delta = delta.p;
-    a3.tp = two_pass;
-    a3.partials = partials.p;
-    a3.n_partials = plan.L3;  // pass A: one partial sum per column n3
     return hipk::launch_pass3(plan, hipk::P3_POWER, a3, nb, stream);
   }
 
@@ -1115,8 +1080,6 @@ int HipEngine::setup_impl(const SearchGeometry& g, const float* host_series, con
   if (wis.persist_per_cu >= 0) d.persist_per_cu = static_cast<uint32_t>(wis.persist_per_cu);
   if (const char* e = std::getenv("BRP_PERSIST")) d.persist_per_cu = static_cast<uint32_t>(std::atoi(e));
   d.plan.persist_wgs = d.persist_per_cu * d.num_cus;
-  d.two_pass = !d.bs && hipk::two_pass_supported(d.plan, g.n_unpadded) && std::getenv("BRP_TWO_PASS") != nullptr &&
-               std::atoi(std::getenv("BRP_TWO_PASS")) != 0;
   log_message(LOG_DEBUG, true, "FFT plan: N=%u M=%u = %u x %u x %u\n", g.nsamples, d.plan.M, d.plan.L1, d.plan.L2,
               d.plan.L3);
   const uint32_t limit = std::min(g.harmonic_idx_hi, g.fft_size);
@@ -1140,7 +1103,10 @@ int HipEngine::setup_impl(const SearchGeometry& g, const float* host_series, con
   if (const char* e = std::getenv("BRP_HS_CAP")) {
     // fault injection (small lists overflow early); never below what the
     // bounded output of a full batch emits (100 per template and level, +28 % for ties)
-    const uint32_t min_cap = static_cast<uint32_t>(d.slot_cap()) * kNumHarmonicLevels * 128u;
+    // (BRP_FAULT=hs_cap_raw: taken as is, so that the bounded output itself
+    // overflows -- the tie-storm path of complete())
+    const uint32_t min_cap =
+        fault_enabled("hs_cap_raw") ? 1u : static_cast<uint32_t>(d.slot_cap()) * kNumHarmonicLevels * 128u;
     d.cap = std::max<uint32_t>(min_cap, static_cast<uint32_t>(std::atol(e)));
     d.kcopy = std::min(d.kcopy, d.cap);
     d.inplace_max = std::min(d.inplace_max, d.kcopy);
@@ -1160,6 +1126,7 @@ int HipEngine::setup_impl(const SearchGeometry& g, const float* host_series, con
     d.inplace_max = std::min<uint32_t>(d.kcopy, static_cast<uint32_t>(std::max(0, std::atoi(e))));
   d.hs_direct = std::getenv("BRP_HS_DIRECT") == nullptr || std::atoi(std::getenv("BRP_HS_DIRECT")) != 0;
   d.hs_xcd = std::getenv("BRP_HS_XCD") != nullptr && std::atoi(std::getenv("BRP_HS_XCD")) == 1;
+  d.lds_pass1 = std::getenv("BRP_P1_LDS") != nullptr && std::atoi(std::getenv("BRP_P1_LDS")) == 1;
   if ((rc = d.pyr.alloc(B * hipk::hs_pyr_stride(d.ps_stride)))) return rc;
   if ((rc = d.partials.alloc(B * d.plan.wg1()))) return rc;  // pass-1 partial sums (P1_RESAMPLE / P1_CHIRP*)
   if (d.bs) {
@@ -1554,7 +1521,10 @@ int HipEngine::submit(const TemplateInput* t, int nb, const float* thr, int thr_
     for (int h = 0; h < kNumHarmonicLevels; ++h) d.h_thr.p[k * hipk::kHsThrStride + h] = th[h];
   }
   hipGraphExec_t exec = nullptr;
-  const int key = nb * Impl::kIoSlots + slot;
+  // captured graphs differ by batch size, I/O slot and output path (compacting
+  // or bounded select): entering or leaving select mode picks the other graph
+  // instead of replaying one of the wrong path
+  const int key = (nb * Impl::kIoSlots + slot) * 2 + (d.select_mode ? 1 : 0);
   auto it = d.graphs.find(key);
   // Direct launches into the stream by default: with two batches in flight the
   // launch cost is hidden, and replaying the batch as a HIP graph measured
@@ -1628,9 +1598,9 @@ int HipEngine::complete(std::vector<TemplateCands>& out) {
                 d.cap, nb);
     int rc;
     if ((rc = d.ensure_select())) return rc;
+    // graphs are keyed by the output path, so none is destroyed here (the next
+    // batch's graph launch may still be queued on the stream)
     d.select_mode = true;
-    for (auto& kv : d.graphs) (void)hipGraphExecDestroy(kv.second);  // captured the compacting path
-    d.graphs.clear();
     d.select_io(slot);
     if (d.fg_in) std::atomic_thread_fence(std::memory_order_seq_cst);
     BRP_HIP_CHECK(d.enqueue(nb), RADPUL_HIP_KERNEL_INVOKE);
@@ -1641,10 +1611,46 @@ int HipEngine::complete(std::vector<TemplateCands>& out) {
     cnt = o.h_cands_p[0].x;
     d.prev_done = nullptr;  // the statistics chain restarts
   }
+  std::vector<uint2> extra;
+  const uint2* src = o.h_cands_p + 1;
   if (cnt > d.cap) {
-    // bounded output overflowing: > cap / 5 equal values at one 100th place
-    log_message(LOG_ERROR, true, "Candidate overflow (%u > %u slots) in a batch of %d templates.\n", cnt, d.cap, nb);
-    return RADPUL_HIP_CAND_OVERFLOW;
+    // The bounded output itself overflowed: more values >= some template's
+    // 100th-largest than list slots, i.e. a storm of exact ties at a 100th
+    // place (the reference keeps inserting them one by one,
+    // demod_binary.c:1310-1397). The bounded output is deterministic and its
+    // counter kept counting past the cap, so one more run of the batch into a
+    // list of exactly `cnt` slots emits every value: no input the reference
+    // accepts ends in RADPUL_HIP_CAND_OVERFLOW.
+    log_message(LOG_DEBUG, true, "Bounded output overflow (%u > %u slots, %d templates): list of %u slots.\n", cnt,
+                d.cap, nb, cnt);
+    DevBuf<uint2> big;
+    int rc;
+    if ((rc = big.alloc(1 + static_cast<size_t>(cnt)))) return rc;
+    const uint32_t cap0 = d.cap;
+    const bool sel0 = d.select_mode;
+    int rc2;
+    if ((rc2 = d.ensure_select())) return rc2;
+    d.select_io(slot);
+    d.cands.p = big.p;  // the list of this run only (the slot's own list is untouched)
+    d.cap = cnt;
+    d.select_mode = true;
+    hipError_t e = d.enqueue(nb);
+    d.cap = cap0;
+    d.select_mode = sel0;
+    d.select_io(slot);
+    BRP_HIP_CHECK(e, RADPUL_HIP_KERNEL_INVOKE);
+    extra.resize(1 + static_cast<size_t>(cnt));
+    BRP_HIP_CHECK(hipMemcpyAsync(extra.data(), big.p, extra.size() * sizeof(uint2), hipMemcpyDeviceToHost, d.stream),
+                  RADPUL_HIP_MEM_COPY_DEVICE_HOST);
+    BRP_HIP_CHECK(hipStreamSynchronize(d.stream), RADPUL_HIP_MEM_COPY_DEVICE_HOST);
+    if (extra[0].x != cnt) {  // the same batch, thresholds and spectrum: cannot differ
+      log_message(LOG_ERROR, true, "Bounded output re-run emitted %u values, the first run %u.\n", extra[0].x, cnt);
+      return RADPUL_HIP_CAND_OVERFLOW;
+    }
+    src = extra.data() + 1;
+    d.st.tie_reruns += 1;
+    d.st.list_dma_copies += 1;
+    d.prev_done = nullptr;
   }
   if (ran_select && d.select_mode && !d.select_forced && o.h_cands_p[0].y <= d.cap / 4) {
     // the thresholds (table floors) rose: the compacting path fits again
@@ -1653,11 +1659,9 @@ int HipEngine::complete(std::vector<TemplateCands>& out) {
   }
   if (ran_select) d.st.select_batches += 1;
   d.st.candidates += cnt;
-  const uint2* src = o.h_cands_p + 1;
-  std::vector<uint2> extra;
   // beyond kcopy entries a DMA copy of the list beats reading it in place
   // (uncached reads over the PCIe BAR) or a second copied prefix
-  if (cnt > (d.fg_out ? d.inplace_max : d.kcopy)) {
+  if (extra.empty() && cnt > (d.fg_out ? d.inplace_max : d.kcopy)) {
     extra.resize(cnt);
     // stream-ordered (a null-stream copy would invalidate another engine's
     // graph capture running in a sibling thread); waits for a batch queued

