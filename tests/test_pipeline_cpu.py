@@ -158,3 +158,8 @@ def test_fft_path_any_length(brp):
         assert 2 * q.dft_len - 1 <= q.conv_len <= 1.2 * (2 * q.dft_len)
         L1, L2, L3 = q.factors
         assert L1 * L2 * L3 == q.conv_len
+    # 7-smooth N/2 (radix-7 plan lengths 112 / 224 / 448): the three-pass FFT,
+    # not a chirp-z transform over >= 2 Mb - 1 (-P 3.5: N = 7 * 2^21)
+    for P, factors in ((3.5, (224, 128, 256)), (6.125, (224, 224, 256))):
+        r = ops.fft_path(int(P * (1 << 22) + 0.5))
+        assert r.kind == "three-pass" and r.work_ratio == 1.0 and r.factors[:3] == factors, (P, r)
