@@ -54,15 +54,24 @@ const uint32_t kPlanP12[] = {512, 448, 384, 320, 288, 256, 240, 224, 192, 160, 1
 // the minimum.
 bool make_bluestein_plan(uint32_t Mb, FFTPlan3& plan) {
   const uint64_t need = 2ull * Mb - 1;
-  uint64_t best = 0;
+  std::vector<uint64_t> lens;
   for (uint32_t L3 : kPlanP3)
     for (uint32_t L1 : kPlanP12)
       for (uint32_t L2 : kPlanP12) {
         if (L2 > L1 || static_cast<uint64_t>(L2) * L3 > kMaxL2L3 || !hipk::pass12_length_supported(L2)) continue;
         const uint64_t L = static_cast<uint64_t>(L1) * L2 * L3;
-        if (L >= need && L < (1ull << 31) && (best == 0 || L < best)) best = L;
+        if (L >= need && L < (1ull << 31)) lens.push_back(L);
       }
-  return best != 0 && make_fft_plan(static_cast<uint32_t>(best), plan);
+  if (lens.empty()) return false;
+  std::sort(lens.begin(), lens.end());
+  lens.erase(std::unique(lens.begin(), lens.end()), lens.end());
+  // the smallest length whose plan runs the transposed convolution
+  // (hipk::chirp_rev_supported), unless that costs more than 3 % in length
+  for (uint64_t L : lens) {
+    if (L > lens.front() + lens.front() / 32) break;
+    if (make_fft_plan(static_cast<uint32_t>(L), plan) && hipk::chirp_rev_supported(plan)) return true;
+  }
+  return make_fft_plan(static_cast<uint32_t>(lens.front()), plan);
 }
 
 bool make_fft_plan(uint32_t M, FFTPlan3& plan) {
@@ -356,6 +365,11 @@ struct HipEngine::Impl {
   uint32_t bs_Mb = 0;
   DevBuf<float2> bs_a;          // [batch][L] chirp-in / convolution spectrum / A
   DevBuf<float2> bs_h;          // [L] FFT_L of the wrapped conjugate chirp
+  // template transforms as the transposed convolution (bluestein_kernels.hpp:
+  // pass3_mid, reverse passes 2 and 1) with H in row layout; BRP_BS_REV=0:
+  // the natural-order form (pass3_cplx, a second forward transform)
+  bool bs_rev = false;
+  DevBuf<float2> bs_hp;         // [L] H in the row layout
   DevBuf<float2> bs_chirp_hi, bs_chirp_lo;  // W_{2 Mb}
   bool ready = false;
   uint32_t num_cus = 256;
@@ -405,6 +419,7 @@ struct HipEngine::Impl {
                                 // 44 KB LDS / 125 VGPRs per workgroup: 16.4-16.7k vs 15.6-15.8k templates/s)
   bool hs_xcd = false;          // pruned HS: contiguous block ranges per XCD (BRP_HS_XCD=1)
   bool lds_pass1 = false;       // resampling pass 1 on the LDS-staged kernel (BRP_P1_LDS=1, A/B)
+  bool mid_rows8 = false;       // pass3_mid: 8 rows per workgroup for every L3 (BRP_MID_ROWS8=1, A/B)
   bool hs_direct = true;        // bounds read straight from global memory (BRP_HS_DIRECT=0: LDS-staged;
                                 // +2 % fp32, +3 % config 5 in one call, profiles/README.md round 3)
   DevBuf<double> partials;      // [batch][wg1]
@@ -528,6 +543,7 @@ struct HipEngine::Impl {
     t.hi = tw_hi.p;
     t.lo = tw_lo.p;
     t.period = 2ull * g.nsamples;  // W_2N (= W_{4M} of the packed transform)
+    t.inv_period = 1.0 / static_cast<double>(t.period);
     return t;
   }
   hipk::TwiddleTable chirpt() const {
@@ -535,6 +551,7 @@ struct HipEngine::Impl {
     t.hi = bs_chirp_hi.p;
     t.lo = bs_chirp_lo.p;
     t.period = 2ull * bs_Mb;
+    t.inv_period = 1.0 / static_cast<double>(t.period);
     return t;
   }
 
@@ -638,7 +655,59 @@ struct HipEngine::Impl {
     return hipk::launch_pass1(plan, m, a1, bs_trans(nb), stream);
   }
   hipError_t bs_template_round0(int nb) {
+    if (bs_rev) {  // forward pass 2 (+ delta), then the middle: rows * H, conj, inverse rows, in place
+      hipk::Pass2Args a2 = bs_pass2_args(plan.wg1(), bs_pair ? 2u : 1u, static_cast<uint32_t>(nb));
+      hipError_t e = hipk::launch_pass2(plan, a2, bs_trans(nb), stream);
+      if (e != hipSuccess) return e;
+      hipk::Pass3MidArgs am{};
+      am.buf = buf.p;
+      am.hp = bs_hp.p;
+      am.L1 = plan.L1;
+      am.L2 = plan.L2;
+      am.L3 = plan.L3;
+      am.tb = tables();
+      am.rows8 = mid_rows8;
+      return hipk::launch_pass3_mid(plan, am, bs_trans(nb), stream);
+    }
     return bs_fft_rest(bs_trans(nb), hipk::C3_MULCONJ, bs_a.p, plan.wg1(), bs_pair ? 2u : 1u, static_cast<uint32_t>(nb));
+  }
+  // the inverse transform's columns in transposed order: reverse pass 2, then
+  // pass 1 with the final chirp into bs_a (A, n < Mb)
+  hipError_t bs_template_round1(int nb) {
+    if (!bs_rev) return bs_round(bs_trans(nb), 1);
+    hipk::Pass2Args a2 = bs_pass2_args(0, 1, 0);
+    a2.rev = true;
+    hipError_t e = hipk::launch_pass2(plan, a2, bs_trans(nb), stream);
+    if (e != hipSuccess) return e;
+    hipk::Pass1Args a1{};
+    a1.out = bs_a.p;
+    a1.L2L3 = plan.L2 * plan.L3;
+    a1.L3 = plan.L3;
+    a1.tw = twt();
+    a1.tb = tables();
+    a1.cplx_in = buf.p;
+    a1.chirp = chirpt();
+    a1.Mb = bs_Mb;
+    a1.scale = static_cast<float>(1.0 / static_cast<double>(plan.M));
+    return hipk::launch_pass1(plan, hipk::P1_REV_CHIRP, a1, bs_trans(nb), stream);
+  }
+  hipk::Pass2Args bs_pass2_args(uint32_t n_partials, uint32_t tpt, uint32_t n_tmpl) {
+    hipk::Pass2Args a2{};
+    a2.buf = buf.p;
+    a2.L1 = plan.L1;
+    a2.L2L3 = plan.L2 * plan.L3;
+    a2.L3 = plan.L3;
+    a2.tw = twt();
+    a2.tb = tables();
+    if (n_partials > 0) {
+      a2.partials = partials.p;
+      a2.n_partials = n_partials;
+      a2.tmpl = tmpl.p;
+      a2.delta = delta.p;
+      a2.tpt = tpt;
+      a2.n_tmpl = n_tmpl;
+    }
+    return a2;
   }
   hipError_t bs_template_power(int nb, float* ps_out, _Float16* ps16_out, uint32_t stride, uint32_t limit) {
     hipk::BsPowerArgs ap{};
@@ -661,7 +730,7 @@ struct HipEngine::Impl {
   hipError_t bs_template_spectra(int nb, float* ps_out, _Float16* ps16_out, uint32_t stride, uint32_t limit) {
     hipError_t e = bs_template_in(nb, nullptr);
     if (e == hipSuccess) e = bs_template_round0(nb);
-    if (e == hipSuccess) e = bs_round(bs_trans(nb), 1);
+    if (e == hipSuccess) e = bs_template_round1(nb);
     return e == hipSuccess ? bs_template_power(nb, ps_out, ps16_out, stride, limit) : e;
   }
 
@@ -749,7 +818,7 @@ struct HipEngine::Impl {
         return fft_pass2(nb);
       case kPass3: {
         if (bs) {
-          const hipError_t e3 = bs_round(bs_trans(nb), 1);
+          const hipError_t e3 = bs_template_round1(nb);
           if (e3 != hipSuccess) return e3;
           return bs_template_power(nb, ps.p, ps_fp16 ? reinterpret_cast<_Float16*>(ps.p) : nullptr, ps_stride,
                                    std::min(g.harmonic_idx_hi, g.fft_size));
@@ -1069,8 +1138,10 @@ int HipEngine::setup_impl(const SearchGeometry& g, const float* host_series, con
       log_message(LOG_ERROR, true, "No FFT plan for length %u.\n", g.nsamples);
       return RADPUL_HIP_FFT_PLAN;
     }
-    log_message(LOG_INFO, true, "FFT length %u: chirp-z transform of length %u over %u = %u x %u x %u points.\n",
-                g.nsamples, d.bs_Mb, d.plan.M, d.plan.L1, d.plan.L2, d.plan.L3);
+    d.bs_rev = hipk::chirp_rev_supported(d.plan) &&
+               (std::getenv("BRP_BS_REV") == nullptr || std::atoi(std::getenv("BRP_BS_REV")) != 0);
+    log_message(LOG_INFO, true, "FFT length %u: chirp-z transform of length %u over %u = %u x %u x %u points%s.\n",
+                g.nsamples, d.bs_Mb, d.plan.M, d.plan.L1, d.plan.L2, d.plan.L3, d.bs_rev ? " (transposed)" : "");
   }
   // measured settings for this (arch, M) from the plan wisdom; environment wins
   const PlanWisdom wis = load_wisdom(wisdom_path(), d.arch, d.plan.M);
@@ -1127,16 +1198,19 @@ int HipEngine::setup_impl(const SearchGeometry& g, const float* host_series, con
   d.hs_direct = std::getenv("BRP_HS_DIRECT") == nullptr || std::atoi(std::getenv("BRP_HS_DIRECT")) != 0;
   d.hs_xcd = std::getenv("BRP_HS_XCD") != nullptr && std::atoi(std::getenv("BRP_HS_XCD")) == 1;
   d.lds_pass1 = std::getenv("BRP_P1_LDS") != nullptr && std::atoi(std::getenv("BRP_P1_LDS")) == 1;
+  d.mid_rows8 = std::getenv("BRP_MID_ROWS8") != nullptr && std::atoi(std::getenv("BRP_MID_ROWS8")) == 1;
   if ((rc = d.pyr.alloc(B * hipk::hs_pyr_stride(d.ps_stride)))) return rc;
   if ((rc = d.partials.alloc(B * d.plan.wg1()))) return rc;  // pass-1 partial sums (P1_RESAMPLE / P1_CHIRP*)
   if (d.bs) {
     if ((rc = d.bs_a.alloc(B * d.plan.M)) || (rc = d.bs_h.alloc(d.plan.M))) return rc;
+    if (d.bs_rev && (rc = d.bs_hp.alloc(d.plan.M))) return rc;
     const auto& ch = twiddles_cached(2ull * d.bs_Mb);
     if ((rc = d.upload(d.bs_chirp_hi, ch.first)) || (rc = d.upload(d.bs_chirp_lo, ch.second))) return rc;
   } else {
     d.bs_a.release();
     d.bs_h.release();
   }
+  if (!d.bs || !d.bs_rev) d.bs_hp.release();
   if ((rc = d.delta.alloc(B))) return rc;
   const size_t BS = static_cast<size_t>(d.slot_cap());  // templates per I/O slot
   d.thr_bytes = (BS * hipk::kHsThrStride * sizeof(float) + 63) / 64 * 64;
@@ -1197,6 +1271,9 @@ int HipEngine::setup_impl(const SearchGeometry& g, const float* host_series, con
   if ((rc = d.build_tables())) return rc;
   if (d.bs) {
     BRP_HIP_CHECK(d.bs_make_h(), RADPUL_HIP_KERNEL_INVOKE);
+    if (d.bs_rev)
+      BRP_HIP_CHECK(hipk::launch_bs_rows(d.bs_h.p, d.bs_hp.p, d.plan.L1, d.plan.L2, d.plan.L3, d.stream),
+                    RADPUL_HIP_KERNEL_INVOKE);
     BRP_HIP_CHECK(hipStreamSynchronize(d.stream), RADPUL_HIP_KERNEL_INVOKE);
   }
   if ((rc = upload_series0(host_series, dev_series, src_device, packed))) return rc;

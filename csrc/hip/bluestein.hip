@@ -132,7 +132,24 @@ __global__ void __launch_bounds__(kThreads) bs_real_out_kernel(const float2* A, 
   }
 }
 
+// H in the row layout of the transposed convolution (Pass3MidArgs):
+// hp[(k1 L2 + k2) L3 + k3] = H[k1 + L1 k2 + L1 L2 k3] (once per plan)
+__global__ void __launch_bounds__(kThreads) bs_rows_kernel(const float2* H, float2* hp, uint32_t L1, uint32_t L2,
+                                                           uint32_t L3) {
+  const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
+  if (i >= L1 * L2 * L3) return;
+  const uint32_t row = i / L3, k3 = i % L3;
+  const uint32_t k1 = row / L2, k2 = row % L2;
+  hp[i] = H[k1 + L1 * k2 + L1 * L2 * k3];
+}
+
 }  // namespace
+
+hipError_t launch_bs_rows(const float2* H, float2* hp, uint32_t L1, uint32_t L2, uint32_t L3, hipStream_t s) {
+  const uint32_t n = L1 * L2 * L3;
+  hipLaunchKernelGGL(bs_rows_kernel, dim3((n + kThreads - 1) / kThreads), dim3(kThreads), 0, s, H, hp, L1, L2, L3);
+  return hipGetLastError();
+}
 
 uint32_t bs_chirp_in_blocks(uint32_t L) { return (L + kThreads * kPerThread - 1) / (kThreads * kPerThread); }
 

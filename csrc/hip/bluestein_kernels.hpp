@@ -12,7 +12,15 @@
 //   y = chirp(a) (zero padded)          bs_chirp_in_kernel (templates: pass 1, P1_CHIRP*)
 //   FFT_L(y) * H -> conj                 pass 1, 2, pass3_cplx (C3_MULCONJ)
 //   FFT_L again -> conj * w / L          pass 1, 2, pass3_cplx (C3_CHIRP)
-// with H = FFT_L(conj chirp, wrapped) precomputed once per plan. The consumers
+// with H = FFT_L(conj chirp, wrapped) precomputed once per plan. The template
+// transforms run the convolution in transposed form instead: the DFT matrix
+// is symmetric, so the inverse's three passes can run in reverse order on the
+// forward transform's row layout --
+//   pass 1 (P1_CHIRP*), pass 2           forward, rows (k1, k2) over n3 left in place
+//   pass3_mid                            row FFT, * H (row layout), conj, row FFT, twiddle
+//   pass 2 (rev), pass 1 (P1_REV_CHIRP)  columns over k2, then k1; conj * w / L, n < Mb
+// -- five passes instead of six, and no natural-order (64-B piece) stores of
+// the spectrum in between (round 5, profiles/README.md). The consumers
 // (power spectrum with the mean-padding correction, whitening spectrum, real
 // output of the inverse) are the bs_*_kernel launchers below.
 #pragma once
@@ -91,6 +99,8 @@ uint32_t bs_chirp_in_blocks(uint32_t L);
 hipError_t launch_pass3_cplx(const FFTPlan3& plan, Pass3CplxMode mode, const Pass3CplxArgs& a, int batch,
                              hipStream_t s);
 hipError_t launch_bs_power(const BsPowerArgs& a, int batch, hipStream_t s);
+// H (natural order) -> the row layout of the transposed convolution (pass3_mid)
+hipError_t launch_bs_rows(const float2* H, float2* hp, uint32_t L1, uint32_t L2, uint32_t L3, hipStream_t s);
 // whitening: A -> complex half spectrum X_k, k < fft_size (unnormalised)
 hipError_t launch_bs_spec(const float2* A, uint32_t Mb, uint32_t nsamples, const TwiddleTable& tw, uint32_t fft_size,
                           float2* spec, hipStream_t s);

@@ -50,6 +50,11 @@ enum Pass1Mode : int {
   // 2p and 2p + 1 of the launch (X_a, X_b separate by conjugate symmetry in
   // bs_power_kernel): half the chirp-z work per template
   P1_CHIRP1_PAIR = 6,
+  // last pass of a chirp-z convolution's inverse transform in transposed
+  // order (bluestein_kernels.hpp): columns over k1 of `cplx_in` (pass 2's
+  // reverse output) -> natural-order n, then conj(.) * w_n * scale for n < Mb
+  // into `out` (the length-Mb DFT A); no output twiddle
+  P1_REV_CHIRP = 7,
 };
 
 struct Pass1Args {
@@ -72,6 +77,7 @@ struct Pass1Args {
   TwiddleTable chirp;
   uint32_t Mb;
   uint32_t n_tmpl;             // P1_CHIRP1_PAIR: templates of the launch (transform p: 2p, 2p + 1 < n_tmpl)
+  float scale;                 // P1_REV_CHIRP: 1 / L
   bool lds_pass1;              // P1_RESAMPLE: LDS-staged pass1_kernel instead of pass1g_kernel (BRP_P1_LDS=1)
 };
 
@@ -91,6 +97,10 @@ struct Pass2Args {
   // 0 counts as 1) and templates of the launch: transform p reduces the
   // partial sums of templates tpt p .. tpt p + tpt - 1 (< n_tmpl)
   uint32_t tpt, n_tmpl;
+  // reverse (transposed) pass of a chirp-z convolution's inverse transform:
+  // DFT over the column's k2 -> m2 with the output twiddle W_{L1 L2}^{k1 m2}
+  // (p1 table) instead of pass 2's W_M^{n3 (k1 + L1 k2)}
+  bool rev;
 };
 
 enum Pass3Mode : int {
@@ -117,6 +127,21 @@ struct Pass3Args {
   float2* spec;                // fft_size complex bins
 };
 
+// Middle of a chirp-z convolution (bluestein_kernels.hpp), in place on the
+// row layout pass 2 leaves: per row (k1, k2) the forward row FFT over n3 ->
+// k3, times H in the same layout (hp[row][k3] = H[k1 + L1 k2 + L1 L2 k3]),
+// conj, the row FFT of the transposed inverse transform (k3 -> m3) and its
+// twiddle W_M^{m3 (k1 + L1 k2)}. Pass 2 (rev) and pass 1 (P1_REV_CHIRP) finish
+// the inverse transform from there, so the convolution never writes the
+// spectrum in natural order.
+struct Pass3MidArgs {
+  float2* buf;                 // [batch][M], in place
+  const float2* hp;            // [M] H in row layout
+  uint32_t L1, L2, L3;
+  FFTTables tb;                // st3; p2col, p2lo, p2hi (the twiddle)
+  bool rows8;                  // 8 rows per workgroup for every L3 (BRP_MID_ROWS8=1, A/B)
+};
+
 // plain row pass of the inverse transform: conj, scale, write the first
 // n_out real samples of the natural-order output
 struct Pass3PlainArgs {
@@ -133,6 +158,9 @@ hipError_t launch_pass1(const FFTPlan3& plan, Pass1Mode mode, const Pass1Args& a
 hipError_t launch_pass2(const FFTPlan3& plan, const Pass2Args& a, int batch, hipStream_t s);
 hipError_t launch_pass3(const FFTPlan3& plan, Pass3Mode mode, const Pass3Args& a, int batch, hipStream_t s);
 hipError_t launch_pass3_plain(const FFTPlan3& plan, const Pass3PlainArgs& a, hipStream_t s);
+hipError_t launch_pass3_mid(const FFTPlan3& plan, const Pass3MidArgs& a, int batch, hipStream_t s);
+// lengths of the transposed chirp-z convolution (pass3_mid, pass 2 rev, P1_REV_CHIRP)
+bool chirp_rev_supported(const FFTPlan3& plan);
 
 // lengths with compiled kernels
 bool pass12_length_supported(uint32_t L);

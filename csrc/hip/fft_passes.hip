@@ -458,7 +458,7 @@ __global__ void __launch_bounds__(kNcol * tpc_for<L>(), kMinWaves) pass2_kernel(
 // times, with two barriers per tile. The output twiddle
 // W_M^{n3 (k1 + L1 k2)} = wc * W_{L2L3}^{n3 tj} * (W_{L2L3}^{n3 TPC})^q is
 // evaluated exactly at q = 0 and q = 8 and stepped by one rotation in between.
-template <int L>
+template <int L, bool REV = false>
 __global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_per_eu(3, 8))) pass2r_kernel(Pass2Args a, uint32_t ntiles) {
   constexpr int R1 = L / 16;
   constexpr int TPC = R1;
@@ -540,6 +540,24 @@ __global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_
 #pragma unroll
     for (int q = 1; q < 16; ++q) y[q] = cmul(y[q], wl[(tj * q) % L]);
     Dft<16>::run(y);
+    if constexpr (REV) {
+      // transposed inverse transform: outputs m2 = tj + TPC q with
+      // W_{L1 L2}^{k1 m2} (p1 table, [m2][k1]), exact at q = 0 and 8 and
+      // stepped by W_{L1 L2}^{k1 TPC} in between (as the forward twiddles)
+      const float2* p1c = a.tb.p1 + k1;
+      const float2 step = p1c[static_cast<uint32_t>(TPC) * a.L1];
+      float2 t0 = p1c[static_cast<uint32_t>(tj) * a.L1];
+      float2 t8 = p1c[static_cast<uint32_t>(tj + 8 * TPC) * a.L1];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        *const_cast<float2*>(at(base, q)) = cmul(y[q], t0);
+        *const_cast<float2*>(at(base, q + 8)) = cmul(y[q + 8], t8);
+        t0 = cmul(t0, step);
+        t8 = cmul(t8, step);
+      }
+      tile = next;
+      continue;
+    }
     // outputs k2 = tj + TPC q
     auto wexact = [&](uint32_t e) { return cmul(hi[e >> kP2LoBits], lo[e & (kLo - 1)]); };
     const float2 step = wexact(n3 * static_cast<uint32_t>(TPC));
@@ -573,7 +591,9 @@ template <> struct RadixSplit<14> { static constexpr int A = 2, B = 7; };
 template <> struct RadixSplit<15> { static constexpr int A = 3, B = 5; };
 template <> struct RadixSplit<18> { static constexpr int A = 2, B = 9; };
 template <> struct RadixSplit<20> { static constexpr int A = 4, B = 5; };
+template <> struct RadixSplit<24> { static constexpr int A = 3, B = 8; };
 template <> struct RadixSplit<28> { static constexpr int A = 4, B = 7; };
+template <> struct RadixSplit<32> { static constexpr int A = 2, B = 16; };
 
 template <int R, class TW>
 __device__ __forceinline__ void dft_any(float2* v, TW tw) {
@@ -605,6 +625,32 @@ __device__ __forceinline__ void dft_any(float2* v, TW tw) {
   }
 }
 
+// Chirp factors w_n = W_{2 Mb}^{n^2 mod 2 Mb} along n_q = n0 + q D: exact at
+// q = 0 and every 8 steps, in between w_{q+1} = w_q * r_q with
+// r_q = W^{2 n_q D + D^2} and r_{q+1} = r_q * W^{2 D^2} (two complex products
+// per element instead of a 64-bit reduction and two scattered table loads:
+// n^2 mod 2 Mb lands anywhere in the table). 7 steps add a few ulp of phase.
+struct ChirpWalk {
+  const TwiddleTable& t;
+  uint64_t n0, D;
+  float2 w, r, c2;
+  __device__ __forceinline__ ChirpWalk(const TwiddleTable& tt, uint64_t n0_, uint64_t D_) : t(tt), n0(n0_), D(D_) {
+    c2 = tw_lookup(t, 2 * D * D);
+  }
+  // w_{n_q}; call with q = 0, 1, 2, ... in order
+  __device__ __forceinline__ float2 next(int q) {
+    if (q % 8 == 0) {
+      const uint64_t n = n0 + static_cast<uint64_t>(q) * D;
+      w = tw_lookup(t, n * n);
+      r = tw_lookup(t, 2 * n * D + D * D);
+    } else {
+      w = cmul(w, r);
+      r = cmul(r, c2);
+    }
+    return w;
+  }
+};
+
 // Register-staged pass 2 for L = 16 * R1 with R1 not a divisor of 16 (96, 144,
 // 160, 192, 240, 288, 320: the chirp-z plans' lengths), two Stockham stages in
 // the other order than pass2r_kernel: radix 16 first (butterfly tj of a column
@@ -613,7 +659,7 @@ __device__ __forceinline__ void dft_any(float2* v, TW tw) {
 // rows k2 = j + 16 q they store). The tile crosses LDS once; the generic
 // LDS-staged kernel crossed it once per stage (measured 22.3 us per million
 // elements at L2 = 288 against 5.4 for pass2r, profiles/kernel_stats_r4.txt).
-template <int L>
+template <int L, bool REV = false>
 __global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_per_eu(2, 8))) pass2g_kernel(Pass2Args a, uint32_t ntiles) {
   constexpr int R1 = L / 16;
   constexpr int TPC = R1;
@@ -693,6 +739,29 @@ __global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_
       }
     }
     __syncthreads();  // LDS tile free for the next tile's stage 1
+    if constexpr (REV) {
+      // transposed inverse transform: outputs m2 = j + 16 q with
+      // W_{L1 L2}^{k1 m2} (p1 table, [m2][k1]), exact every 8 rows and
+      // stepped by W_{L1 L2}^{16 k1} in between (as the forward twiddles)
+      const float2* p1c = a.tb.p1 + k1;
+      const float2 step = p1c[16u * a.L1];
+#pragma unroll
+      for (int v = 0; v < NB2; ++v) {
+        const int j = tj + TPC * v;
+        if (j < 16) {
+          const uint32_t st_off = (static_cast<uint32_t>(j) * a.L3 + c) * sizeof(float2);
+          float2 t = make_float2(1.f, 0.f);
+#pragma unroll
+          for (int q = 0; q < R1; ++q) {
+            if (q % 8 == 0) t = p1c[static_cast<uint32_t>(j + 16 * q) * a.L1];
+            *reinterpret_cast<float2*>(reinterpret_cast<char*>(base + q * st_step) + st_off) = cmul(y[v][q], t);
+            t = cmul(t, step);
+          }
+        }
+      }
+      tile = next;
+      continue;
+    }
     // outputs k2 = j + 16 q with W_M^{n3 (k1 + L1 k2)} = wc * W_{L2L3}^{n3 k2},
     // exact every 8 rows and stepped by W_{L2L3}^{16 n3} in between
     auto wexact = [&](uint32_t e) { return cmul(hi[e >> kP2LoBits], lo[e & (kLo - 1)]); };
@@ -731,7 +800,8 @@ __global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_
   constexpr int TPC = R1;
   constexpr int NB2 = (16 + TPC - 1) / TPC;  // stage-2 butterflies per thread (16 per column)
   constexpr bool kChirp = MODE == P1_CHIRP2 || MODE == P1_CHIRP1 || MODE == P1_CHIRP1_PAIR;
-  static_assert(kChirp || MODE == P1_COMPLEX || MODE == P1_COMPLEX_CONJ || MODE == P1_RESAMPLE, "pass1g modes");
+  static_assert(kChirp || MODE == P1_COMPLEX || MODE == P1_COMPLEX_CONJ || MODE == P1_RESAMPLE || MODE == P1_REV_CHIRP,
+                "pass1g modes");
   constexpr int NT = kNcol * TPC;
   __shared__ __attribute__((aligned(16))) float2 data[L * kNcol];
   __shared__ float2 wl[L];  // W_L^e
@@ -824,22 +894,65 @@ __global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_
       const int i = min(max(fast ? resamp_nearest_f(m, dt) : resamp_nearest(m, dt), 0), last);
       return ser[i] - t.mu0;
     };
-    float fsum = 0.0f, fsum_b = 0.0f;
+    (void)sample_of;
+    // three phases as the resampling gather: the nearest indices of all 16
+    // rows (two samples each: the pair (2n, 2n + 1), or templates a and b),
+    // all loads in flight together, then centring, chirp and the sums
+    const uint32_t n0 = static_cast<uint32_t>(tj) * a.L2L3 + col_base + c;
+    const uint32_t D = static_cast<uint32_t>(R1) * a.L2L3;
+    // rows q >= qw of the whole wave lie in the zero padding (n >= Mb, about
+    // half the rows): their gathers and chirp factors are skipped uniformly
+    const uint32_t qw = wave_max_u32(n0 < a.Mb ? min(16u, (a.Mb - n0 + D - 1) / D) : 0u);
+    int idx[32];
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
-      const uint32_t n = static_cast<uint32_t>(tj + R1 * q) * a.L2L3 + col_base + c;
+      const uint32_t n = n0 + q * D;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const TemplateDev& t = (MODE == P1_CHIRP2 || h == 0) ? td : tdb;
+        const uint32_t m = MODE == P1_CHIRP2 ? 2 * n + h : n;
+        int i = -1;
+        if (n < a.Mb && m < t.n_steps && (MODE == P1_CHIRP2 || h == 0 || has_b)) {
+          const float dt = resamp_del_t(m, t.p, lut_s, lut_c);
+          i = min(max(fast ? resamp_nearest_f(m, dt) : resamp_nearest(m, dt), 0), last);
+        }
+        idx[2 * q + h] = i;
+      }
+    }
+    // loads in two halves of 8 rows; the second only when a row of the wave
+    // needs it (uniform branch: a per-row guard spilled the arrays)
+    float raw[32];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const float* ser = (MODE == P1_CHIRP2 || e % 2 == 0) ? series : series_b;
+      raw[e] = ser[idx[e] < 0 ? 0 : idx[e]];
+    }
+#pragma unroll
+    for (int e = 16; e < 32; ++e) raw[e] = 0.0f;
+    if (qw > 8) {
+#pragma unroll
+      for (int e = 16; e < 32; ++e) {
+        const float* ser = (MODE == P1_CHIRP2 || e % 2 == 0) ? series : series_b;
+        raw[e] = ser[idx[e] < 0 ? 0 : idx[e]];
+      }
+    }
+    float fsum = 0.0f, fsum_b = 0.0f;
+    ChirpWalk cw(a.chirp, n0, D);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
       float2 v = make_float2(0.0f, 0.0f);
-      if (n < a.Mb) {
-        float2 xs;
+      if (static_cast<uint32_t>(q) < qw) {
+        const float2 w = cw.next(q);  // W_{2Mb}^{n^2 mod 2Mb}
+        const float s0 = idx[2 * q] < 0 ? 0.0f : raw[2 * q] - td.mu0;
+        const float s1 = idx[2 * q + 1] < 0 ? 0.0f : raw[2 * q + 1] - (MODE == P1_CHIRP2 ? td.mu0 : tdb.mu0);
+        const float2 xs = make_float2(s0, s1);
         if (MODE == P1_CHIRP2) {
-          xs = make_float2(sample_of(td, series, 2 * n), sample_of(td, series, 2 * n + 1));
           fsum += xs.x + xs.y;
         } else {
-          xs = make_float2(sample_of(td, series, n), has_b ? sample_of(tdb, series_b, n) : 0.0f);
           fsum += xs.x;
           fsum_b += xs.y;
         }
-        v = cmul(xs, tw_lookup(a.chirp, static_cast<uint64_t>(n) * n));  // W_{2Mb}^{n^2 mod 2Mb}
+        if (n0 + q * D < a.Mb) v = cmul(xs, w);
       }
       x[q] = v;
     }
@@ -860,6 +973,8 @@ __global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_
   for (int v = 0; v < NB2; ++v) {
     const int j = tj + TPC * v;
     if (j < 16) {
+      // P1_REV_CHIRP: chirp factors of the outputs n = (j + 16 q) L2L3 + col
+      ChirpWalk cw(a.chirp, static_cast<uint64_t>(j) * a.L2L3 + col_base + c, 16ull * a.L2L3);
       float2 y[R1];
 #pragma unroll
       for (int q = 0; q < R1; ++q) y[q] = data[col(j + 16 * q, c)];
@@ -869,7 +984,14 @@ __global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_
 #pragma unroll
       for (int q = 0; q < R1; ++q) {
         const int k1 = j + 16 * q;
-        out[static_cast<size_t>(k1) * a.L2L3] = cmul(y[q], two[k1]);
+        if constexpr (MODE == P1_REV_CHIRP) {
+          // natural-order n: conj(.) * w_n / L for n < Mb (the length-Mb DFT)
+          const uint32_t n = static_cast<uint32_t>(k1) * a.L2L3 + col_base + c;
+          const float2 w = cw.next(q);
+          if (n < a.Mb) out[static_cast<size_t>(k1) * a.L2L3] = cscale(cmul(conjf2(y[q]), w), a.scale);
+        } else {
+          out[static_cast<size_t>(k1) * a.L2L3] = cmul(y[q], two[k1]);
+        }
       }
     }
   }
@@ -1203,6 +1325,64 @@ __global__ void __launch_bounds__(ROWS * tpc_for<L>()) pass3_cplx_kernel(Pass3Cp
   }
 }
 
+// Middle of the transposed chirp-z convolution (Pass3MidArgs): ROWS
+// consecutive rows of the row layout (row r = k1 L2 + k2 at r L3), forward
+// row FFT, times H (same layout) and conj, second row FFT (the first pass of
+// the transposed inverse transform), twiddle W_M^{m3 (k1 + L1 k2)}, stored
+// back in place. Rows are contiguous in memory: whole-line loads and stores,
+// where the natural-order epilogue of pass3_cplx_kernel wrote 64-B pieces.
+template <int L, int ROWS>
+__global__ void __launch_bounds__(ROWS * tpc_for<L>()) pass3_mid_kernel(Pass3MidArgs a) {
+  constexpr int TPC = tpc_for<L>();
+  constexpr int NT = ROWS * TPC;
+  using Lay = BlockLayout<L, ROWS, TPC, true>;
+  constexpr int kLo = 1 << kP2LoBits;
+  __shared__ __attribute__((aligned(16))) float2 smem[Lay::kLds + kTwPad<L> + kTwRowExtra<L>];
+  float2* data = smem;
+  float2* twl = smem + Lay::kLds;
+  const uint32_t M = a.L1 * a.L2 * a.L3;
+  const uint32_t r0 = blockIdx.x * ROWS;
+  float2* buf = a.buf + static_cast<size_t>(blockIdx.y) * M;
+  int slot, tj;
+  Lay::coords(threadIdx.x, slot, tj);
+  const uint32_t row = r0 + slot;
+  const size_t rbase = static_cast<size_t>(row) * L;
+  constexpr int kPer = L / TPC;
+  static_assert(L % TPC == 0, "whole row iterations");
+  {
+    float2 v[kPer];
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) v[u] = buf[rbase + tj + u * TPC];
+    copy_row_twiddles<L>(twl, a.tb.st3);
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) data[Lay::idx(tj + u * TPC, slot)] = v[u];
+  }
+  __syncthreads();
+  BlockFFT<L, ROWS, TPC, true>::run(data, twl);  // n3 -> k3 (natural order)
+  {
+    float2 h[kPer];
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) h[u] = a.hp[rbase + tj + u * TPC];
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int e = Lay::idx(tj + u * TPC, slot);
+      data[e] = conjf2(cmul(data[e], h[u]));
+    }
+  }
+  __syncthreads();
+  BlockFFT<L, ROWS, TPC, true>::run(data, twl);  // k3 -> m3
+  // W_M^{m3 (k1 + L1 k2)} = W_M^{m3 k1} * W_{L2 L3}^{m3 k2}
+  const uint32_t k1 = row / a.L2, k2 = row % a.L2;
+  const float2* wc = a.tb.p2col + static_cast<size_t>(k1) * L;
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    const uint32_t m3 = tj + u * TPC;
+    const uint32_t e = m3 * k2;
+    const float2 w = cmul(wc[m3], cmul(a.tb.p2hi[e >> kP2LoBits], a.tb.p2lo[e & (kLo - 1)]));
+    buf[rbase + m3] = cmul(data[Lay::idx(m3, slot)], w);
+  }
+}
+
 }  // namespace
 
 // ------------------------------------------------------------ dispatch glue
@@ -1212,6 +1392,12 @@ __global__ void __launch_bounds__(ROWS * tpc_for<L>()) pass3_cplx_kernel(Pass3Cp
   X(16) X(32) X(48) X(64) X(80) X(96) X(112) X(128) X(144) X(160) X(192) X(224) X(240) X(256) X(288) X(320) X(384) \
       X(448) X(512)
 #define BRP_P3_LENGTHS(X) X(64) X(96) X(128) X(160) X(192) X(256) X(320)
+// register-staged pass 2 (pass2r_kernel: R1 | 16; pass2g_kernel: the others)
+#define BRP_P2R_LENGTHS(X) X(32) X(64) X(128) X(256)
+#define BRP_P2G_LENGTHS(X) X(48) X(80) X(96) X(112) X(144) X(160) X(192) X(224) X(240) X(288) X(320) X(448)
+// register-staged pass 1 (pass1g_kernel) of every mode but the resampling gather
+#define BRP_P1G_LENGTHS(X) \
+  X(48) X(64) X(80) X(96) X(112) X(128) X(144) X(160) X(192) X(224) X(240) X(256) X(288) X(320) X(384) X(448) X(512)
 
 bool pass12_length_supported(uint32_t L) {
   switch (L) {
@@ -1252,12 +1438,33 @@ hipError_t launch_pass1(const FFTPlan3& plan, Pass1Mode mode, const Pass1Args& a
   // register-staged pass 1 (one LDS crossing); a.lds_pass1: the LDS-staged
   // pass1_kernel for the resampling gather instead (A/B switch, BRP_P1_LDS=1)
   if (BRP_P1G && mode != P1_REAL && !(mode == P1_RESAMPLE && a.lds_pass1)) {
+    // lengths R1 | 16 and the long ones: complex-input and chirp modes only
+    // (the resampling gather keeps its kernels there: pruned3 / LDS-staged)
+    if (mode != P1_RESAMPLE) {
+      switch (plan.L1) {
+#define X(n)                                                                                                 \
+  case n: {                                                                                                  \
+    const dim3 blk(kNcol * (n / 16));                                                                        \
+    if (mode == P1_COMPLEX) hipLaunchKernelGGL((pass1g_kernel<n, P1_COMPLEX>), grid, blk, 0, s, a);          \
+    else if (mode == P1_COMPLEX_CONJ) hipLaunchKernelGGL((pass1g_kernel<n, P1_COMPLEX_CONJ>), grid, blk, 0, s, a); \
+    else if (mode == P1_CHIRP2) hipLaunchKernelGGL((pass1g_kernel<n, P1_CHIRP2>), grid, blk, 0, s, a);       \
+    else if (mode == P1_CHIRP1) hipLaunchKernelGGL((pass1g_kernel<n, P1_CHIRP1>), grid, blk, 0, s, a);       \
+    else if (mode == P1_REV_CHIRP) hipLaunchKernelGGL((pass1g_kernel<n, P1_REV_CHIRP>), grid, blk, 0, s, a); \
+    else hipLaunchKernelGGL((pass1g_kernel<n, P1_CHIRP1_PAIR>), grid, blk, 0, s, a);                         \
+    return hipGetLastError();                                                                                \
+  }
+        X(48) X(64) X(80) X(128) X(256) X(384) X(512)
+#undef X
+        default: break;
+      }
+    }
     switch (plan.L1) {
 #define X(n)                                                                                         \
   case n: {                                                                                          \
     const dim3 blk(kNcol * (n / 16));                                                                \
     if (mode == P1_RESAMPLE) hipLaunchKernelGGL((pass1g_kernel<n, P1_RESAMPLE>), grid, blk, 0, s, a); \
     else if (mode == P1_COMPLEX) hipLaunchKernelGGL((pass1g_kernel<n, P1_COMPLEX>), grid, blk, 0, s, a); \
+    else if (mode == P1_REV_CHIRP) hipLaunchKernelGGL((pass1g_kernel<n, P1_REV_CHIRP>), grid, blk, 0, s, a); \
     else if (mode == P1_COMPLEX_CONJ) hipLaunchKernelGGL((pass1g_kernel<n, P1_COMPLEX_CONJ>), grid, blk, 0, s, a); \
     else if (mode == P1_CHIRP2) hipLaunchKernelGGL((pass1g_kernel<n, P1_CHIRP2>), grid, blk, 0, s, a);             \
     else if (mode == P1_CHIRP1) hipLaunchKernelGGL((pass1g_kernel<n, P1_CHIRP1>), grid, blk, 0, s, a);             \
@@ -1295,11 +1502,12 @@ hipError_t launch_pass2(const FFTPlan3& plan, const Pass2Args& a, int batch, hip
   // register-staged pass 2 where compiled (one LDS crossing per tile), the
   // generic LDS-staged kernel for the other lengths
   switch (plan.L2) {
-#define X(n)                                                                                   \
-  case n:                                                                                      \
-    hipLaunchKernelGGL((pass2r_kernel<n>), grid, dim3(kNcol * (n / 16)), 0, s, a, ntiles);     \
+#define X(n)                                                                                       \
+  case n:                                                                                          \
+    if (a.rev) hipLaunchKernelGGL((pass2r_kernel<n, true>), grid, dim3(kNcol * (n / 16)), 0, s, a, ntiles); \
+    else hipLaunchKernelGGL((pass2r_kernel<n>), grid, dim3(kNcol * (n / 16)), 0, s, a, ntiles);   \
     return hipGetLastError();
-    X(32) X(64) X(128) X(256)
+    BRP_P2R_LENGTHS(X)
 #undef X
     default: break;
   }
@@ -1308,17 +1516,19 @@ hipError_t launch_pass2(const FFTPlan3& plan, const Pass2Args& a, int batch, hip
 #ifndef BRP_P2G
 #define BRP_P2G 1
 #endif
-  if (BRP_P2G) {
+  if (BRP_P2G || a.rev) {
     switch (plan.L2) {
-#define X(n)                                                                                 \
-  case n:                                                                                    \
-    hipLaunchKernelGGL((pass2g_kernel<n>), grid, dim3(kNcol * (n / 16)), 0, s, a, ntiles);     \
+#define X(n)                                                                                       \
+  case n:                                                                                          \
+    if (a.rev) hipLaunchKernelGGL((pass2g_kernel<n, true>), grid, dim3(kNcol * (n / 16)), 0, s, a, ntiles); \
+    else hipLaunchKernelGGL((pass2g_kernel<n>), grid, dim3(kNcol * (n / 16)), 0, s, a, ntiles);   \
     return hipGetLastError();
-      X(96) X(112) X(144) X(160) X(192) X(224) X(240) X(288) X(320) X(448)
+      BRP_P2G_LENGTHS(X)
 #undef X
       default: break;
     }
   }
+  if (a.rev) return hipErrorInvalidValue;  // no reverse form of the LDS-staged kernel
   switch (plan.L2) {
 #define X(n)                                                                \
   case n:                                                                   \
@@ -1369,6 +1579,61 @@ hipError_t launch_pass3_cplx(const FFTPlan3& plan, Pass3CplxMode mode, const Pas
     else if (mode == C3_MULCONJ) hipLaunchKernelGGL((pass3_cplx_kernel<n, kRows3, C3_MULCONJ>), grid, block, 0, s, a); \
     else hipLaunchKernelGGL((pass3_cplx_kernel<n, kRows3, C3_CHIRP>), grid, block, 0, s, a);                     \
     break;                                                                                                         \
+  }
+    BRP_P3_LENGTHS(X)
+#undef X
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+bool chirp_rev_supported(const FFTPlan3& plan) {
+  bool l1 = false, l2 = false, l3 = false;
+  switch (plan.L1) {
+#define X(n) case n:
+    BRP_P1G_LENGTHS(X)
+#undef X
+    l1 = true;
+    default: break;
+  }
+  switch (plan.L2) {
+#define X(n) case n:
+    BRP_P2R_LENGTHS(X) BRP_P2G_LENGTHS(X)
+#undef X
+    l2 = true;
+    default: break;
+  }
+  switch (plan.L3) {
+#define X(n) case n:
+    BRP_P3_LENGTHS(X)
+#undef X
+    l3 = true;
+    default: break;
+  }
+  return l1 && l2 && l3 && BRP_P1G;
+}
+
+// rows per pass3_mid workgroup: whole waves (8 rows of L / 16 threads where
+// that is a multiple of 64, else 16 or 32); a.rows8: always 8 (A/B switch)
+template <int L>
+constexpr int mid_rows() {
+  return (8 * tpc_for<L>()) % kWave == 0 ? 8 : (16 * tpc_for<L>()) % kWave == 0 ? 16 : 32;
+}
+
+hipError_t launch_pass3_mid(const FFTPlan3& plan, const Pass3MidArgs& a, int batch, hipStream_t s) {
+  const uint32_t rows = plan.L1 * plan.L2;
+  switch (plan.L3) {
+#define X(n)                                                                                              \
+  case n: {                                                                                               \
+    constexpr int R = mid_rows<n>();                                                                      \
+    if (a.rows8 || R == 8) {                                                                              \
+      if (rows % 8 != 0) return hipErrorInvalidValue;                                                     \
+      hipLaunchKernelGGL((pass3_mid_kernel<n, 8>), dim3(rows / 8, batch), dim3(8 * tpc_for<n>()), 0, s, a); \
+    } else {                                                                                              \
+      if (rows % R != 0) return hipErrorInvalidValue;                                                     \
+      hipLaunchKernelGGL((pass3_mid_kernel<n, R>), dim3(rows / R, batch), dim3(R * tpc_for<n>()), 0, s, a); \
+    }                                                                                                     \
+    break;                                                                                                \
   }
     BRP_P3_LENGTHS(X)
 #undef X

@@ -32,6 +32,9 @@ struct TwiddleTable {
   const float2* hi;
   const float2* lo;
   uint64_t period;  // 2N
+  // 1 / period (tw_lookup's reduction by a double-precision reciprocal; 0:
+  // the plain 64-bit modulo). Set by the host for every table (periods < 2^32).
+  double inv_period = 0.0;
 };
 
 #if defined(__HIP__)
@@ -45,8 +48,23 @@ __device__ __forceinline__ float2 conjf2(float2 a) { return make_float2(a.x, -a.
 __device__ __forceinline__ float2 mul_mi(float2 a) { return make_float2(a.y, -a.x); }
 __device__ __forceinline__ float2 cscale(float2 a, float s) { return make_float2(a.x * s, a.y * s); }
 
+// j mod m (m < 2^32, j < 2^60) from a double-precision quotient estimate,
+// corrected exactly: gfx950 has no 64-bit integer divide, and the compiler's
+// 64-bit urem is a ~100-instruction sequence per call -- measured as most of
+// the chirp-z kernels' arithmetic (n^2 mod 2 Mb per element, round 5). The
+// estimate q is within a few units of j / m (one rounding of j and of the
+// product), so the two loops run at most a couple of times.
+__device__ __forceinline__ uint32_t mod_u64(uint64_t j, uint32_t m, double inv_m) {
+  const uint64_t q = static_cast<uint64_t>(static_cast<double>(j) * inv_m);
+  int64_t r = static_cast<int64_t>(j - q * m);
+  while (r < 0) r += m;
+  while (r >= static_cast<int64_t>(m)) r -= m;
+  return static_cast<uint32_t>(r);
+}
+
 __device__ __forceinline__ float2 tw_lookup(const TwiddleTable& t, uint64_t j) {
-  j %= t.period;
+  if (t.inv_period != 0.0 && j < (1ull << 60)) j = mod_u64(j, static_cast<uint32_t>(t.period), t.inv_period);
+  else j %= t.period;
   const float2 a = t.hi[j >> kTwLoBits];
   const float2 b = t.lo[j & ((1u << kTwLoBits) - 1)];
   return cmul(a, b);
@@ -66,6 +84,13 @@ __device__ __forceinline__ uint32_t xcd_remap(uint32_t bid, uint32_t nwg) {
   constexpr uint32_t kXcd = 8;
   const uint32_t q = nwg / kXcd, r = nwg % kXcd, x = bid % kXcd, k = bid / kXcd;
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
+}
+
+// wave-level maximum (64 lanes) of a uint32, uniform result
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = max(v, static_cast<uint32_t>(__shfl_xor(static_cast<int>(v), off, 64)));
+  return __builtin_amdgcn_readfirstlane(v);
 }
 
 // wave-level sum (64 lanes) of a double

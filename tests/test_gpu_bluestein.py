@@ -182,14 +182,21 @@ def test_odd_length_template_pairs_match_single(brp, gpu, tmp_path, monkeypatch)
 
 
 # (samples, padding) whose chirp-z plans put every length of the
-# register-staged passes (fft_passes.hip pass1g_kernel for L1, pass2g_kernel
-# for L2: 96, 144, 160, 192, 240, 288, 320) in place at least once
-# (found with derive_geometry + brp.bluestein_plan; the plan is asserted below)
+# register-staged passes in place at least once: pass1g_kernel for L1 (48 ...
+# 512, forward P1_CHIRP* and the transposed inverse's P1_REV_CHIRP), pass 2
+# for L2 forward and reversed (pass2r_kernel 32 / 64 / 128 / 256,
+# pass2g_kernel 48 ... 320; L2 = 448 needs 2^22 samples), pass3_mid_kernel for L3; (65536, 1.53) has
+# L2 = 16 and runs the natural-order convolution (no reverse pass 2 there).
+# Found with derive_geometry + brp.bluestein_plan; the plan is asserted below.
 _REG_CASES = [
-    (1 << 16, 5.01, (144, 48)), (1 << 16, 6.26, (96, 48)), (1 << 17, 7.51, (144, 144)), (1 << 17, 8.46, (96, 96)),
-    (1 << 18, 5.63, (240, 80)), (1 << 18, 6.02, (160, 80)), (1 << 19, 5.87, (192, 128)), (1 << 19, 6.01, (160, 160)),
-    (1 << 19, 7.51, (288, 144)), (1 << 19, 8.44, (240, 240)), (1 << 19, 8.8, (192, 192)), (1 << 20, 6.04, (320, 160)),
-    (1 << 20, 7.54, (288, 288)), (1 << 21, 6.02, (320, 320)),
+    (1 << 16, 1.53, (112, 16)), (1 << 16, 1.58, (48, 48)), (1 << 16, 3.95, (64, 32)), (1 << 16, 5.01, (144, 48)),
+    (1 << 16, 6.01, (112, 112)), (1 << 16, 6.58, (96, 48)), (1 << 16, 7.51, (80, 80)), (1 << 16, 7.89, (64, 64)),
+    (1 << 17, 7.51, (144, 144)), (1 << 17, 7.82, (112, 96)), (1 << 17, 7.88, (128, 64)), (1 << 18, 5.63, (240, 80)),
+    (1 << 18, 6.13, (160, 80)), (1 << 18, 7.88, (128, 128)), (1 << 18, 9.02, (224, 112)), (1 << 19, 5.08, (192, 112)),
+    (1 << 19, 6.15, (160, 160)), (1 << 19, 7.51, (288, 144)), (1 << 19, 7.9, (256, 128)), (1 << 19, 8.76, (240, 240)),
+    (1 << 19, 8.8, (192, 192)), (1 << 19, 9.01, (224, 224)), (1 << 20, 6.13, (320, 160)), (1 << 20, 7.54, (288, 288)),
+    (1 << 20, 7.88, (256, 256)), (1 << 20, 9.03, (448, 224)), (1 << 21, 5.07, (384, 224)), (1 << 21, 6.14, (320, 320)),
+    (1 << 21, 7.89, (512, 256)),
 ]
 
 
