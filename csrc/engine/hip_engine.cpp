@@ -43,7 +43,10 @@ namespace brp {
 using hipk::TemplateDev;
 
 namespace {
-constexpr uint64_t kMaxL2L3 = 256ull * 512;  // W_{L2 L3} as lo[256] x hi[512] (build_tables)
+// W_{L2 L3} as lo[256] x hi[1024] (build_tables): L2 L3 <= 2^18, so that the
+// chirp-z convolution of the longest odd N (P = 10 at 2^22 samples: L >= 84 M)
+// has a plan (512 x 2^17 = 67 M was the limit before round 5)
+constexpr uint64_t kMaxL2L3 = 256ull * 1024;
 const uint32_t kPlanP3[] = {256, 320, 192, 160, 128, 96, 64};
 const uint32_t kPlanP12[] = {512, 448, 384, 320, 288, 256, 240, 224, 192, 160, 144, 128, 112, 96, 80, 64, 48, 32, 16};
 }  // namespace
@@ -55,6 +58,8 @@ const uint32_t kPlanP12[] = {512, 448, 384, 320, 288, 256, 240, 224, 192, 160, 1
 bool make_bluestein_plan(uint32_t Mb, FFTPlan3& plan) {
   const uint64_t need = 2ull * Mb - 1;
   std::vector<uint64_t> lens;
+  // BRP_BS_L3 (A/B): only convolution lengths whose plan has this row length
+  const uint32_t want_l3 = std::getenv("BRP_BS_L3") ? static_cast<uint32_t>(std::atoi(std::getenv("BRP_BS_L3"))) : 0;
   for (uint32_t L3 : kPlanP3)
     for (uint32_t L1 : kPlanP12)
       for (uint32_t L2 : kPlanP12) {
@@ -67,11 +72,30 @@ bool make_bluestein_plan(uint32_t Mb, FFTPlan3& plan) {
   lens.erase(std::unique(lens.begin(), lens.end()), lens.end());
   // the smallest length whose plan runs the transposed convolution
   // (hipk::chirp_rev_supported), unless that costs more than 3 % in length
-  for (uint64_t L : lens) {
-    if (L > lens.front() + lens.front() / 32) break;
-    if (make_fft_plan(static_cast<uint32_t>(L), plan) && hipk::chirp_rev_supported(plan)) return true;
+  if (want_l3) {
+    for (uint64_t L : lens)
+      if (make_fft_plan(static_cast<uint32_t>(L), plan) && plan.L3 == want_l3 && hipk::chirp_rev_supported(plan))
+        return true;
   }
-  return make_fft_plan(static_cast<uint32_t>(lens.front()), plan);
+  // Among the lengths up to 20 % above the shortest, the lowest modelled cost
+  // of a plan that runs the transposed convolution (hipk::chirp_rev_supported):
+  // L times 1.15 when the row length L3 takes three LDS stages (96, 160, 192,
+  // 320) rather than two (64, 128, 256). Measured in one call (round 5):
+  // -P 2.9 3 566 templates/s over 256 x 192 x 256 against 3 107 over the
+  // 2.4 % shorter 240 x 160 x 320; -P 2.7 3 402 vs 3 219 (2.9 % longer).
+  double best_cost = 0.0;
+  uint64_t best = 0;
+  for (uint64_t L : lens) {
+    if (L > lens.front() + lens.front() / 5) break;
+    if (!make_fft_plan(static_cast<uint32_t>(L), plan) || !hipk::chirp_rev_supported(plan)) continue;
+    const bool two_stage = plan.L3 == 64 || plan.L3 == 128 || plan.L3 == 256;
+    const double cost = static_cast<double>(L) * (two_stage ? 1.0 : 1.15);
+    if (best == 0 || cost < best_cost) {
+      best = L;
+      best_cost = cost;
+    }
+  }
+  return make_fft_plan(static_cast<uint32_t>(best ? best : lens.front()), plan);
 }
 
 bool make_fft_plan(uint32_t M, FFTPlan3& plan) {
@@ -88,7 +112,7 @@ bool make_fft_plan(uint32_t M, FFTPlan3& plan) {
       const uint32_t L2 = R / L1;
       if (!hipk::pass12_length_supported(L2)) continue;
       if (L1 < L2) continue;
-      if (static_cast<uint64_t>(L2) * L3 > kMaxL2L3) continue;  // pass-2 twiddle table (256 x 512)
+      if (static_cast<uint64_t>(L2) * L3 > kMaxL2L3) continue;  // pass-2 twiddle table (256 x 1024)
       if (!best1 || (L1 - L2) < (best1 - best2)) {
         best1 = L1;
         best2 = L2;
@@ -284,8 +308,8 @@ const HostTables& host_tables(const FFTPlan3& plan) {
     for (uint32_t n3 = 0; n3 < L3; ++n3) h->p2col[k1 * L3 + n3] = root(static_cast<uint64_t>(n3) * k1, M);
   h->p2lo.assign(256, make_float2(0, 0));
   for (uint32_t i = 0; i < 256; ++i) h->p2lo[i] = root(i, L2L3);
-  h->p2hi.assign(512, make_float2(0, 0));
-  for (uint32_t i = 0; i < 512 && 256ull * i < L2L3; ++i) h->p2hi[i] = root(256ull * i, L2L3);
+  h->p2hi.assign(1024, make_float2(0, 0));
+  for (uint32_t i = 0; i < 1024 && 256ull * i < L2L3; ++i) h->p2hi[i] = root(256ull * i, L2L3);
   // pass 3: W_{4 L3}^j = hi[j >> 5] * lo[j & 31], stored as [lo 32 | hi 4 L3 / 32]
   h->p3.assign(32 + 4ull * L3 / 32, make_float2(0, 0));
   for (uint32_t i = 0; i < 32; ++i) h->p3[i] = root(i, 4ull * L3);
@@ -419,7 +443,7 @@ struct HipEngine::Impl {
                                 // 44 KB LDS / 125 VGPRs per workgroup: 16.4-16.7k vs 15.6-15.8k templates/s)
   bool hs_xcd = false;          // pruned HS: contiguous block ranges per XCD (BRP_HS_XCD=1)
   bool lds_pass1 = false;       // resampling pass 1 on the LDS-staged kernel (BRP_P1_LDS=1, A/B)
-  bool mid_rows8 = false;       // pass3_mid: 8 rows per workgroup for every L3 (BRP_MID_ROWS8=1, A/B)
+  bool mid_waves = false;       // pass3_mid: whole-wave workgroups of 16 / 32 rows (BRP_MID_WAVES=1, A/B)
   bool hs_direct = true;        // bounds read straight from global memory (BRP_HS_DIRECT=0: LDS-staged;
                                 // +2 % fp32, +3 % config 5 in one call, profiles/README.md round 3)
   DevBuf<double> partials;      // [batch][wg1]
@@ -666,7 +690,7 @@ struct HipEngine::Impl {
       am.L2 = plan.L2;
       am.L3 = plan.L3;
       am.tb = tables();
-      am.rows8 = mid_rows8;
+      am.whole_waves = mid_waves;
       return hipk::launch_pass3_mid(plan, am, bs_trans(nb), stream);
     }
     return bs_fft_rest(bs_trans(nb), hipk::C3_MULCONJ, bs_a.p, plan.wg1(), bs_pair ? 2u : 1u, static_cast<uint32_t>(nb));
@@ -1198,7 +1222,7 @@ int HipEngine::setup_impl(const SearchGeometry& g, const float* host_series, con
   d.hs_direct = std::getenv("BRP_HS_DIRECT") == nullptr || std::atoi(std::getenv("BRP_HS_DIRECT")) != 0;
   d.hs_xcd = std::getenv("BRP_HS_XCD") != nullptr && std::atoi(std::getenv("BRP_HS_XCD")) == 1;
   d.lds_pass1 = std::getenv("BRP_P1_LDS") != nullptr && std::atoi(std::getenv("BRP_P1_LDS")) == 1;
-  d.mid_rows8 = std::getenv("BRP_MID_ROWS8") != nullptr && std::atoi(std::getenv("BRP_MID_ROWS8")) == 1;
+  d.mid_waves = std::getenv("BRP_MID_WAVES") != nullptr && std::atoi(std::getenv("BRP_MID_WAVES")) == 1;
   if ((rc = d.pyr.alloc(B * hipk::hs_pyr_stride(d.ps_stride)))) return rc;
   if ((rc = d.partials.alloc(B * d.plan.wg1()))) return rc;  // pass-1 partial sums (P1_RESAMPLE / P1_CHIRP*)
   if (d.bs) {

@@ -70,45 +70,89 @@ __device__ __forceinline__ float2 bs_bin(const float2* A, uint32_t Mb, uint32_t 
   return untangle_w(zk, zm, tw_lookup(tw, 2ull * k));  // W_N^k = W_2N^{2k}
 }
 
+// Each thread handles kPowBins consecutive bins k: W_2N^k and W_2N^{n_s k}
+// (the padding correction) are looked up exactly for the first and stepped by
+// one complex product per bin after it (one 64-bit reduction and table pair
+// per kPowBins bins instead of two per bin: n_s k mod 2N lands anywhere in the
+// table). Stores of the bins are contiguous per thread.
+constexpr int kPowBins = 4;
+
 template <bool HALF>
 __global__ void __launch_bounds__(kThreads) bs_power_kernel(BsPowerArgs a) {
   const int b = blockIdx.y;  // transform
-  const uint32_t k = blockIdx.x * kThreads + threadIdx.x;
-  if (k >= a.limit) return;
+  const uint32_t k0 = (blockIdx.x * kThreads + threadIdx.x) * kPowBins;
+  if (k0 >= a.limit) return;
   const uint32_t real_bins = a.nsamples / 2 + 1;  // bins the real DFT defines
-  const bool live = k > 0 && k < real_bins;
   const float2* A = a.A + static_cast<size_t>(b) * a.L;
+  // per template: W_2N^{k0}, W_2N^{n_s k0} and their per-bin steps
+  struct Walk {
+    float2 tk, ta, sk, sa;
+    float dS;
+    uint32_t n_s;
+  };
+  auto walk = [&](uint32_t t) {
+    Walk w{};
+    w.n_s = a.tmpl[t].n_steps;
+    if (w.n_s > 0) {
+      w.dS = static_cast<float>(a.delta[t]);
+      w.tk = tw_lookup(a.tw, k0);
+      w.sk = tw_lookup(a.tw, 1);
+      w.ta = tw_lookup(a.tw, static_cast<uint64_t>(w.n_s) * k0);
+      w.sa = tw_lookup(a.tw, w.n_s);
+    }
+    return w;
+  };
   // X_k (+ delta * S_k, S_k the transform of the padding indicator) -> |.|^2 / N
-  auto power = [&](float2 x, uint32_t t) {
-    const uint32_t n_s = a.tmpl[t].n_steps;
-    if (n_s > 0) {
-      const float dS = static_cast<float>(a.delta[t]);
-      const float2 tk = tw_lookup(a.tw, k);
-      const float2 ta = tw_lookup(a.tw, static_cast<uint64_t>(n_s) * k);
-      const float2 sp = padding_spectrum_t(ta, tk, cmul(ta, conjf2(tk)));  // tc = W_2N^{(n_s - 1) k}
-      x = make_float2(x.x + dS * sp.x, x.y + dS * sp.y);
+  auto power = [&](float2 x, const Walk& w) {
+    if (w.n_s > 0) {
+      const float2 sp = padding_spectrum_t(w.ta, w.tk, cmul(w.ta, conjf2(w.tk)));  // tc = W_2N^{(n_s - 1) k}
+      x = make_float2(x.x + w.dS * sp.x, x.y + w.dS * sp.y);
     }
     return (x.x * x.x + x.y * x.y) * a.norm;
   };
-  auto store = [&](uint32_t t, float p) {
+  auto advance = [](Walk& w) {
+    if (w.n_s > 0) {
+      w.tk = cmul(w.tk, w.sk);
+      w.ta = cmul(w.ta, w.sa);
+    }
+  };
+  auto store = [&](uint32_t t, uint32_t k, float p) {
     const size_t o = static_cast<size_t>(t) * a.ps_stride + k;
     if (HALF) a.ps16[o] = static_cast<_Float16>(fminf(p, 65504.0f));  // saturate: no inf in the fp16 spectrum
     else a.ps[o] = p;
   };
   if (!a.pair) {
-    store(b, live ? power(bs_bin(A, a.Mb, a.nsamples, a.tw, k), b) : 0.0f);
+    Walk w = walk(b);
+#pragma unroll
+    for (int i = 0; i < kPowBins; ++i) {
+      const uint32_t k = k0 + i;
+      if (k >= a.limit) break;
+      const bool live = k > 0 && k < real_bins;
+      store(b, k, live ? power(bs_bin(A, a.Mb, a.nsamples, a.tw, k), w) : 0.0f);
+      advance(w);
+    }
     return;
   }
   // odd N, A = DFT of x_a + i x_b: X_a = (A_k + conj A_{N-k}) / 2, X_b = -i (A_k - conj A_{N-k}) / 2
   const uint32_t ta = 2 * b, tb = 2 * b + 1;
-  float pa = 0.0f, pb = 0.0f;
-  if (live) {
-    const float2 ak = A[k], am = conjf2(A[a.nsamples - k]);
-    pa = power(make_float2(0.5f * (ak.x + am.x), 0.5f * (ak.y + am.y)), ta);
-    if (tb < a.n_tmpl) pb = power(make_float2(0.5f * (ak.y - am.y), -0.5f * (ak.x - am.x)), tb);
+  const bool has_b = tb < a.n_tmpl;
+  Walk wa = walk(ta), wb = has_b ? walk(tb) : Walk{};
+#pragma unroll
+  for (int i = 0; i < kPowBins; ++i) {
+    const uint32_t k = k0 + i;
+    if (k >= a.limit) break;
+    const bool live = k > 0 && k < real_bins;
+    float pa = 0.0f, pb = 0.0f;
+    if (live) {
+      const float2 ak = A[k], am = conjf2(A[a.nsamples - k]);
+      pa = power(make_float2(0.5f * (ak.x + am.x), 0.5f * (ak.y + am.y)), wa);
+      if (has_b) pb = power(make_float2(0.5f * (ak.y - am.y), -0.5f * (ak.x - am.x)), wb);
+    }
+    store(ta, k, pa);
+    if (has_b) store(tb, k, pb);
+    advance(wa);
+    advance(wb);
   }
-  store(ta, pa);
-  if (tb < a.n_tmpl) store(tb, pb);
 }
 
 __global__ void __launch_bounds__(kThreads) bs_spec_kernel(const float2* A, uint32_t Mb, uint32_t N, TwiddleTable tw,
@@ -171,7 +215,7 @@ hipError_t launch_bs_chirp_in(BsInMode mode, const BsInArgs& a, int batch, uint3
 }
 
 hipError_t launch_bs_power(const BsPowerArgs& a, int batch, hipStream_t s) {
-  const dim3 grid((a.limit + kThreads - 1) / kThreads, batch);
+  const dim3 grid((a.limit + kThreads * kPowBins - 1) / (kThreads * kPowBins), batch);
   if (a.ps16) hipLaunchKernelGGL((bs_power_kernel<true>), grid, dim3(kThreads), 0, s, a);
   else hipLaunchKernelGGL((bs_power_kernel<false>), grid, dim3(kThreads), 0, s, a);
   return hipGetLastError();

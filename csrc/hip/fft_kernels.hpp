@@ -32,7 +32,7 @@ struct FFTTables {
   const float2* p1;     // [L2][L1]  W_{L1 L2}^{n2 k1}
   const float2* p2col;  // [L1][L3]  W_M^{n3 k1}
   const float2* p2lo;   // [256]     W_{L2 L3}^{i}
-  const float2* p2hi;   // [<=512]   W_{L2 L3}^{256 i}
+  const float2* p2hi;   // [<=1024]  W_{L2 L3}^{256 i}
   const float2* p3;     // [4 L3]    W_2N^{C i}
 };
 
@@ -139,7 +139,7 @@ struct Pass3MidArgs {
   const float2* hp;            // [M] H in row layout
   uint32_t L1, L2, L3;
   FFTTables tb;                // st3; p2col, p2lo, p2hi (the twiddle)
-  bool rows8;                  // 8 rows per workgroup for every L3 (BRP_MID_ROWS8=1, A/B)
+  bool whole_waves;            // 16 / 32 rows per workgroup where 8 rows are not whole waves (BRP_MID_WAVES=1, A/B)
 };
 
 // plain row pass of the inverse transform: conj, scale, write the first

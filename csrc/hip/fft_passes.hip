@@ -387,7 +387,7 @@ __global__ void __launch_bounds__(kNcol * tpc_for<L>(), kMinWaves) pass2_kernel(
   constexpr int kPer = L / TPC;
   using Lay = BlockLayout<L, kNcol, TPC, false>;
   constexpr int kLo = 1 << kP2LoBits;
-  constexpr int kHiMax = 512;  // L2*L3 <= 2^17
+  constexpr int kHiMax = 1024;  // L2*L3 <= 2^18
   // data | stage twiddles | W_{L2L3} lo | W_{L2L3} hi
   __shared__ __attribute__((aligned(16))) float2 smem[Lay::kLds + kTwPad<L> + kLo + kHiMax];
   __shared__ double red[NT / kWave + 1];
@@ -1371,15 +1371,20 @@ __global__ void __launch_bounds__(ROWS * tpc_for<L>()) pass3_mid_kernel(Pass3Mid
   }
   __syncthreads();
   BlockFFT<L, ROWS, TPC, true>::run(data, twl);  // k3 -> m3
-  // W_M^{m3 (k1 + L1 k2)} = W_M^{m3 k1} * W_{L2 L3}^{m3 k2}
+  // W_M^{m3 (k1 + L1 k2)} = W_M^{m3 k1} (p2col, contiguous in m3) *
+  // W_{L2 L3}^{m3 k2}, the latter exact every 8 elements and stepped by
+  // W_{L2 L3}^{TPC k2} in between (as pass 2's twiddles)
   const uint32_t k1 = row / a.L2, k2 = row % a.L2;
   const float2* wc = a.tb.p2col + static_cast<size_t>(k1) * L;
+  auto wexact = [&](uint32_t e) { return cmul(a.tb.p2hi[e >> kP2LoBits], a.tb.p2lo[e & (kLo - 1)]); };
+  const float2 step = wexact(static_cast<uint32_t>(TPC) * k2);
+  float2 t = make_float2(1.f, 0.f);
 #pragma unroll
   for (int u = 0; u < kPer; ++u) {
     const uint32_t m3 = tj + u * TPC;
-    const uint32_t e = m3 * k2;
-    const float2 w = cmul(wc[m3], cmul(a.tb.p2hi[e >> kP2LoBits], a.tb.p2lo[e & (kLo - 1)]));
-    buf[rbase + m3] = cmul(data[Lay::idx(m3, slot)], w);
+    if (u % 8 == 0) t = wexact(m3 * k2);
+    buf[rbase + m3] = cmul(data[Lay::idx(m3, slot)], cmul(wc[m3], t));
+    t = cmul(t, step);
   }
 }
 
@@ -1394,7 +1399,7 @@ __global__ void __launch_bounds__(ROWS * tpc_for<L>()) pass3_mid_kernel(Pass3Mid
 #define BRP_P3_LENGTHS(X) X(64) X(96) X(128) X(160) X(192) X(256) X(320)
 // register-staged pass 2 (pass2r_kernel: R1 | 16; pass2g_kernel: the others)
 #define BRP_P2R_LENGTHS(X) X(32) X(64) X(128) X(256)
-#define BRP_P2G_LENGTHS(X) X(48) X(80) X(96) X(112) X(144) X(160) X(192) X(224) X(240) X(288) X(320) X(448)
+#define BRP_P2G_LENGTHS(X) X(48) X(80) X(96) X(112) X(144) X(160) X(192) X(224) X(240) X(288) X(320) X(384) X(448) X(512)
 // register-staged pass 1 (pass1g_kernel) of every mode but the resampling gather
 #define BRP_P1G_LENGTHS(X) \
   X(48) X(64) X(80) X(96) X(112) X(128) X(144) X(160) X(192) X(224) X(240) X(256) X(288) X(320) X(384) X(448) X(512)
@@ -1613,8 +1618,10 @@ bool chirp_rev_supported(const FFTPlan3& plan) {
   return l1 && l2 && l3 && BRP_P1G;
 }
 
-// rows per pass3_mid workgroup: whole waves (8 rows of L / 16 threads where
-// that is a multiple of 64, else 16 or 32); a.rows8: always 8 (A/B switch)
+// rows per pass3_mid workgroup: 8 (measured best: -P 2.7 3 151 vs 2 683
+// templates/s with whole-wave workgroups of 16 rows for L3 = 320, and 2 901
+// for a register-staged row FFT, round 5); a.whole_waves: 16 or 32 rows where
+// 8 rows of L / 16 threads are not whole waves (A/B switch)
 template <int L>
 constexpr int mid_rows() {
   return (8 * tpc_for<L>()) % kWave == 0 ? 8 : (16 * tpc_for<L>()) % kWave == 0 ? 16 : 32;
@@ -1626,7 +1633,7 @@ hipError_t launch_pass3_mid(const FFTPlan3& plan, const Pass3MidArgs& a, int bat
 #define X(n)                                                                                              \
   case n: {                                                                                               \
     constexpr int R = mid_rows<n>();                                                                      \
-    if (a.rows8 || R == 8) {                                                                              \
+    if (!a.whole_waves || R == 8) {                                                                       \
       if (rows % 8 != 0) return hipErrorInvalidValue;                                                     \
       hipLaunchKernelGGL((pass3_mid_kernel<n, 8>), dim3(rows / 8, batch), dim3(8 * tpc_for<n>()), 0, s, a); \
     } else {                                                                                              \

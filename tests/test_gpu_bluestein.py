@@ -185,18 +185,23 @@ def test_odd_length_template_pairs_match_single(brp, gpu, tmp_path, monkeypatch)
 # register-staged passes in place at least once: pass1g_kernel for L1 (48 ...
 # 512, forward P1_CHIRP* and the transposed inverse's P1_REV_CHIRP), pass 2
 # for L2 forward and reversed (pass2r_kernel 32 / 64 / 128 / 256,
-# pass2g_kernel 48 ... 320; L2 = 448 needs 2^22 samples), pass3_mid_kernel for L3; (65536, 1.53) has
-# L2 = 16 and runs the natural-order convolution (no reverse pass 2 there).
-# Found with derive_geometry + brp.bluestein_plan; the plan is asserted below.
+# pass2g_kernel 48 ... 320; 384 ... 512 need more than 2^21 samples),
+# pass3_mid_kernel for every L3. Plans with L1 or L2 = 16 (e.g. 1.13 and 1.53
+# at 2^16) run the natural-order convolution. Found with derive_geometry +
+# brp.bluestein_plan (the cost model of make_bluestein_plan); asserted below.
 _REG_CASES = [
-    (1 << 16, 1.53, (112, 16)), (1 << 16, 1.58, (48, 48)), (1 << 16, 3.95, (64, 32)), (1 << 16, 5.01, (144, 48)),
-    (1 << 16, 6.01, (112, 112)), (1 << 16, 6.58, (96, 48)), (1 << 16, 7.51, (80, 80)), (1 << 16, 7.89, (64, 64)),
-    (1 << 17, 7.51, (144, 144)), (1 << 17, 7.82, (112, 96)), (1 << 17, 7.88, (128, 64)), (1 << 18, 5.63, (240, 80)),
-    (1 << 18, 6.13, (160, 80)), (1 << 18, 7.88, (128, 128)), (1 << 18, 9.02, (224, 112)), (1 << 19, 5.08, (192, 112)),
-    (1 << 19, 6.15, (160, 160)), (1 << 19, 7.51, (288, 144)), (1 << 19, 7.9, (256, 128)), (1 << 19, 8.76, (240, 240)),
-    (1 << 19, 8.8, (192, 192)), (1 << 19, 9.01, (224, 224)), (1 << 20, 6.13, (320, 160)), (1 << 20, 7.54, (288, 288)),
-    (1 << 20, 7.88, (256, 256)), (1 << 20, 9.03, (448, 224)), (1 << 21, 5.07, (384, 224)), (1 << 21, 6.14, (320, 320)),
-    (1 << 21, 7.89, (512, 256)),
+    (1 << 16, 1.03, (48, 16, 96)), (1 << 16, 1.13, (16, 16, 320)), (1 << 16, 1.53, (112, 16, 64)),
+    (1 << 16, 1.78, (48, 16, 160)), (1 << 16, 1.33, (48, 48, 96)), (1 << 16, 1.7, (112, 16, 128)),
+    (1 << 16, 1.76, (48, 32, 192)), (1 << 16, 3.39, (64, 32, 256)), (1 << 16, 4.51, (80, 32, 256)),
+    (1 << 16, 5.01, (144, 48, 96)), (1 << 16, 6.01, (112, 112, 64)), (1 << 16, 7.51, (64, 64, 256)),
+    (1 << 16, 8.01, (96, 48, 256)), (1 << 17, 6.13, (80, 80, 256)), (1 << 17, 7.51, (128, 64, 256)),
+    (1 << 17, 8.76, (96, 96, 256)), (1 << 18, 6.13, (160, 80, 256)), (1 << 18, 7.88, (128, 128, 256)),
+    (1 << 18, 9.02, (240, 80, 256)), (1 << 19, 5.01, (144, 144, 256)), (1 << 19, 5.08, (192, 112, 256)),
+    (1 << 19, 6.01, (224, 112, 256)), (1 << 19, 6.15, (160, 160, 256)), (1 << 19, 7.9, (256, 128, 256)),
+    (1 << 19, 8.76, (192, 192, 256)), (1 << 20, 5.04, (288, 144, 256)), (1 << 20, 6.04, (224, 224, 256)),
+    (1 << 20, 6.13, (320, 160, 256)), (1 << 20, 7.88, (256, 256, 256)), (1 << 21, 7.01, (240, 240, 256)),
+    (1 << 21, 5.02, (288, 288, 256)), (1 << 21, 5.07, (384, 224, 256)), (1 << 21, 6.02, (448, 224, 256)),
+    (1 << 21, 6.14, (320, 320, 256)), (1 << 21, 7.89, (512, 256, 256)),
 ]
 
 
@@ -210,7 +215,7 @@ def test_register_staged_pass_lengths(brp, gpu, tmp_path, monkeypatch, n, paddin
     _, series, geom = _geom(brp, tmp_path, n, padding)
     N = geom["nsamples"]
     plan = brp.bluestein_plan(N if N % 2 else N // 2)
-    assert plan is not None and (plan[1], plan[2]) == l12, (N, plan)
+    assert plan is not None and tuple(plan[1:4]) == l12, (N, plan)
     eng = brp.HipEngine()
     eng.init(0, 2)
     eng.setup(geom, series, float(np.mean(series)))

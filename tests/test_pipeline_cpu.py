@@ -158,6 +158,13 @@ def test_fft_path_any_length(brp):
         assert 2 * q.dft_len - 1 <= q.conv_len <= 1.2 * (2 * q.dft_len)
         L1, L2, L3 = q.factors
         assert L1 * L2 * L3 == q.conv_len
+    # every padding on a 0.01 grid of [1, 10] at the benchmark's 2^22 samples and at
+    # a non-power-of-two sample count has a device plan (odd N up to ~84 M points
+    # needs L2 L3 up to 2^18 in the chirp-z convolution)
+    for n_u in (1 << 22, 3 * (1 << 20) + 7):
+        for k in range(901):
+            n = int(float(np.float32(1.0 + 0.01 * k)) * n_u + 0.5)
+            assert ops.fft_path(n).kind in ("three-pass", "chirp-z"), n
     # 7-smooth N/2 (radix-7 plan lengths 112 / 224 / 448): the three-pass FFT,
     # not a chirp-z transform over >= 2 Mb - 1 (-P 3.5: N = 7 * 2^21)
     for P, factors in ((3.5, (224, 128, 256)), (6.125, (224, 224, 256))):
