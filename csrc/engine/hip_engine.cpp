@@ -13,6 +13,7 @@
 #include <atomic>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -72,6 +73,21 @@ bool make_bluestein_plan(uint32_t Mb, FFTPlan3& plan) {
   lens.erase(std::unique(lens.begin(), lens.end()), lens.end());
   // the smallest length whose plan runs the transposed convolution
   // (hipk::chirp_rev_supported), unless that costs more than 3 % in length
+  // BRP_BS_PLAN=L1xL2xL3 (A/B): that factorisation when it covers the length
+  if (const char* e = std::getenv("BRP_BS_PLAN")) {
+    unsigned a1 = 0, a2 = 0, a3 = 0;
+    if (std::sscanf(e, "%ux%ux%u", &a1, &a2, &a3) == 3 && static_cast<uint64_t>(a1) * a2 * a3 >= need &&
+        hipk::pass12_length_supported(a1) && hipk::pass12_length_supported(a2) && hipk::pass3_length_supported(a3)) {
+      plan = FFTPlan3();
+      plan.M = a1 * a2 * a3;
+      plan.L1 = a1;
+      plan.L2 = a2;
+      plan.L3 = a3;
+      plan.ncol1 = plan.ncol2 = 16;
+      plan.rows3 = 8;
+      return true;
+    }
+  }
   if (want_l3) {
     for (uint64_t L : lens)
       if (make_fft_plan(static_cast<uint32_t>(L), plan) && plan.L3 == want_l3 && hipk::chirp_rev_supported(plan))
