@@ -660,7 +660,10 @@ struct ChirpWalk {
 // LDS-staged kernel crossed it once per stage (measured 22.3 us per million
 // elements at L2 = 288 against 5.4 for pass2r, profiles/kernel_stats_r4.txt).
 template <int L, bool REV = false>
-__global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_per_eu(2, 8))) pass2g_kernel(Pass2Args a, uint32_t ntiles) {
+#ifndef BRP_P2G_WAVES
+#define BRP_P2G_WAVES 2  // minimum waves per SIMD the register budget must allow (build switch)
+#endif
+__global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_per_eu(BRP_P2G_WAVES, 8))) pass2g_kernel(Pass2Args a, uint32_t ntiles) {
   constexpr int R1 = L / 16;
   constexpr int TPC = R1;
   constexpr int NT = kNcol * TPC;
@@ -795,7 +798,10 @@ __global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_
 // W_{L1 L2}^{n2 k1}. The LDS-staged pass1_kernel crosses LDS once per stage
 // and bounds the chirp-z transforms (profiles/README.md, round 4).
 template <int L, int MODE>
-__global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_per_eu(2, 8))) pass1g_kernel(Pass1Args a) {
+#ifndef BRP_P1G_WAVES
+#define BRP_P1G_WAVES 2  // minimum waves per SIMD the register budget must allow (build switch)
+#endif
+__global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_per_eu(BRP_P1G_WAVES, 8))) pass1g_kernel(Pass1Args a) {
   constexpr int R1 = L / 16;
   constexpr int TPC = R1;
   constexpr int NB2 = (16 + TPC - 1) / TPC;  // stage-2 butterflies per thread (16 per column)
