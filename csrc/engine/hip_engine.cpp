@@ -410,12 +410,6 @@ struct HipEngine::Impl {
   // the natural-order form (pass3_cplx, a second forward transform)
   bool bs_rev = false;
   DevBuf<float2> bs_hp;         // [L] H in the row layout
-  // chirp-z pass 1 reads the centred resampled series from a pre-pass
-  // (hipk::launch_resample_centred) instead of gathering it itself: the
-  // resampling arithmetic runs at full occupancy there (BRP_BS_PRERES=0: off)
-  bool bs_preres = false;
-  DevBuf<float> bs_y;           // [batch][ystride]
-  uint32_t bs_ystride = 0;
   DevBuf<float2> bs_chirp_hi, bs_chirp_lo;  // W_{2 Mb}
   bool ready = false;
   uint32_t num_cus = 256;
@@ -697,21 +691,6 @@ struct HipEngine::Impl {
     a1.chirp = chirpt();
     a1.Mb = bs_Mb;
     a1.n_tmpl = static_cast<uint32_t>(nb);
-    if (bs_preres) {
-      hipk::ResampCentredArgs r{};
-      r.series = series_in();
-      r.n_unpadded = g.n_unpadded;
-      r.tmpl = tmpl.p;
-      r.y = bs_y.p;
-      r.ystride = bs_ystride;
-      r.n_out = g.nsamples;
-      r.partials = partials.p;
-      r.n_partials = plan.wg1();
-      hipError_t e = hipk::launch_resample_centred(r, nb, stream);
-      if (e != hipSuccess) return e;
-      a1.y = bs_y.p;
-      a1.ystride = bs_ystride;
-    }
     const hipk::Pass1Mode m = bs_pair ? hipk::P1_CHIRP1_PAIR : (bs_Mb == g.nsamples ? hipk::P1_CHIRP1 : hipk::P1_CHIRP2);
     return hipk::launch_pass1(plan, m, a1, bs_trans(nb), stream);
   }
@@ -1265,9 +1244,6 @@ int HipEngine::setup_impl(const SearchGeometry& g, const float* host_series, con
   if (d.bs) {
     if ((rc = d.bs_a.alloc(B * d.plan.M)) || (rc = d.bs_h.alloc(d.plan.M))) return rc;
     if (d.bs_rev && (rc = d.bs_hp.alloc(d.plan.M))) return rc;
-    d.bs_preres = std::getenv("BRP_BS_PRERES") == nullptr || std::atoi(std::getenv("BRP_BS_PRERES")) != 0;
-    d.bs_ystride = (g.nsamples + 63) / 64 * 64;
-    if (d.bs_preres && (rc = d.bs_y.alloc(B * d.bs_ystride))) return rc;
     const auto& ch = twiddles_cached(2ull * d.bs_Mb);
     if ((rc = d.upload(d.bs_chirp_hi, ch.first)) || (rc = d.upload(d.bs_chirp_lo, ch.second))) return rc;
   } else {
@@ -1275,7 +1251,6 @@ int HipEngine::setup_impl(const SearchGeometry& g, const float* host_series, con
     d.bs_h.release();
   }
   if (!d.bs || !d.bs_rev) d.bs_hp.release();
-  if (!d.bs || !d.bs_preres) d.bs_y.release();
   if ((rc = d.delta.alloc(B))) return rc;
   const size_t BS = static_cast<size_t>(d.slot_cap());  // templates per I/O slot
   d.thr_bytes = (BS * hipk::kHsThrStride * sizeof(float) + 63) / 64 * 64;

@@ -78,11 +78,6 @@ struct Pass1Args {
   uint32_t Mb;
   uint32_t n_tmpl;             // P1_CHIRP1_PAIR: templates of the launch (transform p: 2p, 2p + 1 < n_tmpl)
   float scale;                 // P1_REV_CHIRP: 1 / L
-  // P1_CHIRP*: the centred resampled series of the launch's templates
-  // (launch_resample_centred: [template][ystride], zero from n_steps on)
-  // instead of the gather in this pass; the pre-pass wrote the partial sums
-  const float* y;
-  uint32_t ystride;
   bool lds_pass1;              // P1_RESAMPLE: LDS-staged pass1_kernel instead of pass1g_kernel (BRP_P1_LDS=1)
 };
 

@@ -901,32 +901,6 @@ __global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_
       return ser[i] - t.mu0;
     };
     (void)sample_of;
-    if (a.y != nullptr) {
-      // the resampled, centred series from the pre-pass (resample_centred):
-      // coalesced loads of the rows below Mb, the chirp stepped along them
-      const uint32_t n0 = static_cast<uint32_t>(tj) * a.L2L3 + col_base + c;
-      const uint32_t D = static_cast<uint32_t>(R1) * a.L2L3;
-      const uint32_t qw = wave_max_u32(n0 < a.Mb ? min(16u, (a.Mb - n0 + D - 1) / D) : 0u);
-      const float* ya = a.y + static_cast<size_t>(ta) * a.ystride;
-      const float* yb = a.y + static_cast<size_t>(has_b ? ta + 1 : ta) * a.ystride;
-      float2 xs[16];
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        xs[q] = make_float2(0.0f, 0.0f);
-        const uint32_t n = n0 + q * D;
-        if (static_cast<uint32_t>(q) < qw && n < a.Mb) {
-          if (MODE == P1_CHIRP2) xs[q] = *reinterpret_cast<const float2*>(ya + 2 * n);
-          else xs[q] = make_float2(ya[n], has_b ? yb[n] : 0.0f);
-        }
-      }
-      ChirpWalk cw(a.chirp, n0, D);
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        float2 v = make_float2(0.0f, 0.0f);
-        if (static_cast<uint32_t>(q) < qw) v = cmul(xs[q], cw.next(q));
-        x[q] = v;
-      }
-    } else {
     // three phases as the resampling gather: the nearest indices of all 16
     // rows (two samples each: the pair (2n, 2n + 1), or templates a and b),
     // all loads in flight together, then centring, chirp and the sums
@@ -990,7 +964,6 @@ __global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_
     }
     sum = static_cast<double>(fsum);
     sum_b = static_cast<double>(fsum_b);
-    }  // gather in this pass
   }
   for (int e = threadIdx.x; e < L; e += NT) wl[e] = a.tb.st1[e + (e >> 4)];
   // stage 1 (radix 16, Ns = 1): butterfly tj, outputs rows 16 tj + q
@@ -1028,7 +1001,6 @@ __global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_
       }
     }
   }
-  if (kChirp && a.y != nullptr) return;  // the pre-pass wrote the partial sums
   if constexpr (MODE == P1_CHIRP2 || MODE == P1_CHIRP1 || MODE == P1_RESAMPLE) {
     const double tot = block_sum<NT>(sum, red);
     if (threadIdx.x == 0) a.partials[static_cast<size_t>(b) * gridDim.x + blockIdx.x] = tot;

@@ -58,65 +58,7 @@ __global__ void resample_kernel(const float* series, uint32_t n_unpadded, const 
   out[m] = v;
 }
 
-// 4 consecutive samples per thread and step (one float4 store), the
-// workgroup's chunk a multiple of 1024 samples; all 4 gathers in flight together
-__global__ void __launch_bounds__(kThreads) resample_centred_kernel(ResampCentredArgs a) {
-  __shared__ float lut_s[kLutSize], lut_c[kLutSize];
-  __shared__ double red[kThreads / kWave + 1];
-  for (int i = threadIdx.x; i < kLutSize; i += kThreads) {
-    lut_s[i] = kSinLut[i];
-    lut_c[i] = kCosLut[i];
-  }
-  __syncthreads();
-  const uint32_t t = blockIdx.y;
-  const TemplateDev td = a.tmpl[t];
-  const float* series = a.series + static_cast<size_t>(td.wu) * a.n_unpadded;
-  float* y = a.y + static_cast<size_t>(t) * a.ystride;
-  const bool fast = a.n_unpadded <= (1u << 23);
-  const int last = static_cast<int>(a.n_unpadded) - 1;
-  const uint32_t chunk = ((a.n_out + gridDim.x - 1) / gridDim.x + 1023) / 1024 * 1024;
-  const uint32_t lo = blockIdx.x * chunk, hi = min(lo + chunk, a.n_out);
-  float fsum = 0.0f;
-  for (uint32_t m0 = lo + 4 * threadIdx.x; m0 < hi; m0 += 4 * kThreads) {
-    int idx[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const uint32_t m = m0 + e;
-      int i = -1;
-      if (m < td.n_steps && m < hi) {
-        const float dt = resamp_del_t(m, td.p, lut_s, lut_c);
-        i = min(max(fast ? resamp_nearest_f(m, dt) : resamp_nearest(m, dt), 0), last);
-      }
-      idx[e] = i;
-    }
-    float raw[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) raw[e] = series[idx[e] < 0 ? 0 : idx[e]];
-    float v[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      v[e] = idx[e] < 0 ? 0.0f : raw[e] - td.mu0;
-      fsum += v[e];
-    }
-    if (m0 + 4 <= a.ystride) *reinterpret_cast<float4*>(y + m0) = make_float4(v[0], v[1], v[2], v[3]);
-  }
-  double sum = wave_sum(static_cast<double>(fsum));
-  if (threadIdx.x % kWave == 0) red[threadIdx.x / kWave] = sum;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double tot = 0.0;
-    for (int w = 0; w < kThreads / kWave; ++w) tot += red[w];
-    a.partials[static_cast<size_t>(t) * a.n_partials + blockIdx.x] = tot;
-  }
-}
-
 }  // namespace
-
-hipError_t launch_resample_centred(const ResampCentredArgs& a, int templates, hipStream_t s) {
-  if (a.ystride % 4 != 0 || a.ystride < a.n_out) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(resample_centred_kernel, dim3(a.n_partials, templates), dim3(kThreads), 0, s, a);
-  return hipGetLastError();
-}
 
 hipError_t launch_nsteps(TemplateDev* tmpl, int batch, hipStream_t s, uint32_t* reset) {
   hipLaunchKernelGGL(nsteps_kernel, dim3(batch), dim3(kThreads), 0, s, tmpl, reset);
