@@ -194,8 +194,19 @@ def launch_ranks(args) -> int:
 
     n = args.gpus
     if not args.cpu:
+        need = 1 if share_device() else n
         have = visible_gpus()
-        if have < (1 if share_device() else n):
+        if have < need:
+            # second opinion from the runtime, in a child process (this parent
+            # must stay free of HIP): the sysfs view can miss devices on hosts
+            # that expose them differently
+            try:
+                r = subprocess.run([sys.executable, "-c", "import torch; print(torch.cuda.device_count())"],
+                                   capture_output=True, text=True, timeout=300)
+                have = max(have, int(r.stdout.strip().splitlines()[-1]))
+            except (OSError, ValueError, IndexError, subprocess.SubprocessError):
+                pass
+        if have < need:
             print(f"[bench] error: --gpus {n} but only {have} HIP device(s) are visible", file=sys.stderr)
             return 2
     with socket.socket() as s:
