@@ -40,11 +40,11 @@ struct Dft<3> {
   static __device__ __forceinline__ void run(float2* v) {
     const float s = 0.86602540378443864676f;  // sin(2pi/3)
     const float2 t1 = cadd(v[1], v[2]);
-    const float2 t2 = make_float2(v[0].x - 0.5f * t1.x, v[0].y - 0.5f * t1.y);
-    const float2 t3 = mul_mi(cscale(csub(v[1], v[2]), s));
+    const float2 t2 = cfma(-0.5f, t1, v[0]);
+    const float2 d = csub(v[1], v[2]);
     v[0] = cadd(v[0], t1);
-    v[1] = cadd(t2, t3);
-    v[2] = csub(t2, t3);
+    v[1] = add_mi(t2, d, s);  // t2 + (-i) s d
+    v[2] = sub_mi(t2, d, s);
   }
 };
 
@@ -52,11 +52,11 @@ template <>
 struct Dft<4> {
   static __device__ __forceinline__ void run(float2* v) {
     const float2 a0 = cadd(v[0], v[2]), a1 = csub(v[0], v[2]);
-    const float2 b0 = cadd(v[1], v[3]), b1 = mul_mi(csub(v[1], v[3]));
+    const float2 b0 = cadd(v[1], v[3]), d = csub(v[1], v[3]);
     v[0] = cadd(a0, b0);
-    v[1] = cadd(a1, b1);
+    v[1] = add_mi(a1, d);  // a1 + (-i) d
     v[2] = csub(a0, b0);
-    v[3] = csub(a1, b1);
+    v[3] = sub_mi(a1, d);
   }
 };
 
@@ -68,15 +68,15 @@ struct Dft<5> {
     const float2 a1 = cadd(v[1], v[4]), a2 = cadd(v[2], v[3]);
     const float2 b1 = csub(v[1], v[4]), b2 = csub(v[2], v[3]);
     const float2 x0 = v[0];
-    const float2 p1 = make_float2(x0.x + c1 * a1.x + c2 * a2.x, x0.y + c1 * a1.y + c2 * a2.y);
-    const float2 p2 = make_float2(x0.x + c2 * a1.x + c1 * a2.x, x0.y + c2 * a1.y + c1 * a2.y);
-    const float2 q1 = mul_mi(make_float2(s1 * b1.x + s2 * b2.x, s1 * b1.y + s2 * b2.y));
-    const float2 q2 = mul_mi(make_float2(s2 * b1.x - s1 * b2.x, s2 * b1.y - s1 * b2.y));
-    v[0] = make_float2(x0.x + a1.x + a2.x, x0.y + a1.y + a2.y);
-    v[1] = cadd(p1, q1);
-    v[4] = csub(p1, q1);
-    v[2] = cadd(p2, q2);
-    v[3] = csub(p2, q2);
+    const float2 p1 = cfma(c2, a2, cfma(c1, a1, x0));
+    const float2 p2 = cfma(c1, a2, cfma(c2, a1, x0));
+    const float2 q1 = cfma(s2, b2, cscale(b1, s1));   // (-i) q1 is added below
+    const float2 q2 = cfma(-s1, b2, cscale(b1, s2));
+    v[0] = cadd(x0, cadd(a1, a2));
+    v[1] = add_mi(p1, q1);
+    v[4] = sub_mi(p1, q1);
+    v[2] = add_mi(p2, q2);
+    v[3] = sub_mi(p2, q2);
   }
 };
 
@@ -92,23 +92,19 @@ struct Dft<7> {
     const float2 a1 = cadd(v[1], v[6]), a2 = cadd(v[2], v[5]), a3 = cadd(v[3], v[4]);
     const float2 b1 = csub(v[1], v[6]), b2 = csub(v[2], v[5]), b3 = csub(v[3], v[4]);
     const float2 x0 = v[0];
-    auto lin = [](float2 o, float ka, float2 a, float kb, float2 b, float kc, float2 c) {
-      return make_float2(o.x + ka * a.x + kb * b.x + kc * c.x, o.y + ka * a.y + kb * b.y + kc * c.y);
-    };
-    const float2 z = make_float2(0.0f, 0.0f);
-    const float2 p1 = lin(x0, c1, a1, c2, a2, c3, a3);
-    const float2 p2 = lin(x0, c2, a1, c3, a2, c1, a3);
-    const float2 p3 = lin(x0, c3, a1, c1, a2, c2, a3);
-    const float2 q1 = mul_mi(lin(z, s1, b1, s2, b2, s3, b3));
-    const float2 q2 = mul_mi(lin(z, s2, b1, -s3, b2, -s1, b3));
-    const float2 q3 = mul_mi(lin(z, s3, b1, -s1, b2, s2, b3));
-    v[0] = make_float2(x0.x + a1.x + a2.x + a3.x, x0.y + a1.y + a2.y + a3.y);
-    v[1] = cadd(p1, q1);
-    v[6] = csub(p1, q1);
-    v[2] = cadd(p2, q2);
-    v[5] = csub(p2, q2);
-    v[3] = cadd(p3, q3);
-    v[4] = csub(p3, q3);
+    const float2 p1 = cfma(c3, a3, cfma(c2, a2, cfma(c1, a1, x0)));
+    const float2 p2 = cfma(c1, a3, cfma(c3, a2, cfma(c2, a1, x0)));
+    const float2 p3 = cfma(c2, a3, cfma(c1, a2, cfma(c3, a1, x0)));
+    const float2 q1 = cfma(s3, b3, cfma(s2, b2, cscale(b1, s1)));
+    const float2 q2 = cfma(-s1, b3, cfma(-s3, b2, cscale(b1, s2)));
+    const float2 q3 = cfma(s2, b3, cfma(-s1, b2, cscale(b1, s3)));
+    v[0] = cadd(x0, cadd(cadd(a1, a2), a3));
+    v[1] = add_mi(p1, q1);
+    v[6] = sub_mi(p1, q1);
+    v[2] = add_mi(p2, q2);
+    v[5] = sub_mi(p2, q2);
+    v[3] = add_mi(p3, q3);
+    v[4] = sub_mi(p3, q3);
   }
 };
 
@@ -120,10 +116,10 @@ struct Dft<8> {
     float2 o[4] = {v[1], v[3], v[5], v[7]};
     Dft<4>::run(e);
     Dft<4>::run(o);
-    // o[k] *= W8^k
-    o[1] = make_float2(r * (o[1].x + o[1].y), r * (o[1].y - o[1].x));
+    // o[k] *= W8^k: W8 = r (1 - i), W8^2 = -i, W8^3 = r (-1 - i)
+    o[1] = cscale(add_mi(o[1], o[1]), r);                       // r (o.x + o.y, o.y - o.x)
     o[2] = mul_mi(o[2]);
-    o[3] = make_float2(r * (o[3].y - o[3].x), -r * (o[3].x + o[3].y));
+    o[3] = cscale(add_mi(make_float2(-o[3].x, -o[3].y), o[3]), r);  // r (o.y - o.x, -o.x - o.y)
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       v[k] = cadd(e[k], o[k]);
@@ -408,12 +404,29 @@ __device__ __forceinline__ double block_sum(double v, double* scratch) {
   return t;
 }
 
-// X_k of the real FFT from Z_k, Z_{M-k} of the packed complex FFT and w = W_N^k.
+// a * conj(b) as packed operations (the conjugate's sign folds into the
+// instruction instead of a v_xor)
+__device__ __forceinline__ float2 cmulc(float2 a, float2 b) {
+  const f2v av = vec(a), bv = vec(b);
+  const f2v bc = {bv.x, -bv.y};
+  return unvec(av.xx * bc + av.yy * bv.yx);
+}
+
+// X_k of the real FFT from Z_k, Z_{M-k} of the packed complex FFT and w = W_N^k:
+// e = (Z_k + conj Z_{M-k}) / 2, o = (Z_k - conj Z_{M-k}) / 2, X_k = e - i w o
 __device__ __forceinline__ float2 untangle_w(float2 zk, float2 zmk, float2 w) {
-  const float2 bc = conjf2(zmk);
-  const float2 e = cscale(cadd(zk, bc), 0.5f);
-  const float2 o = cscale(csub(zk, bc), 0.5f);
-  return cadd(e, mul_mi(cmul(w, o)));
+  const f2v h = 0.5f * vec(zk), m = vec(zmk);
+  const float2 e = unvec(__builtin_elementwise_fma(m, f2v{0.5f, -0.5f}, h));
+  const float2 o = unvec(__builtin_elementwise_fma(m, f2v{-0.5f, 0.5f}, h));
+  return add_mi(e, cmul(w, o));
+}
+// the mirror bin M - k from the same pair: untangle_w(Z_{M-k}, Z_k, W_N^{M-k})
+// with W_N^{M-k} = -conj(W_N^k): e' + i conj(w) o'
+__device__ __forceinline__ float2 untangle_wm(float2 zmk, float2 zk, float2 w) {
+  const f2v h = 0.5f * vec(zmk), m = vec(zk);
+  const float2 e = unvec(__builtin_elementwise_fma(m, f2v{0.5f, -0.5f}, h));
+  const float2 o = unvec(__builtin_elementwise_fma(m, f2v{-0.5f, 0.5f}, h));
+  return sub_mi(e, cmulc(o, w));
 }
 
 // FFT of the padding indicator 1[m >= n_s] (m < N) at bin k in [1, N/2]:

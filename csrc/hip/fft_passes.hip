@@ -1053,10 +1053,12 @@ struct P3Emit {
     if (k == 0) return 0.0f;
     if (correct) {
       const float ratio = ta.y * __builtin_amdgcn_rcpf(tk.y);  // v_rcp_f32 (1 ulp)
-      const float2 tc = cmul(ta, conjf2(tk));                  // W_2N^{(n_s-1) k}
-      x = make_float2(x.x - dS * ratio * tc.x, x.y - dS * ratio * tc.y);
+      const float2 tc = cmulc(ta, tk);                         // W_2N^{(n_s-1) k}
+      x = cfma(-dS * ratio, tc, x);
     }
-    return (x.x * x.x + x.y * x.y) * a.norm;
+    const f2v xv = vec(x);
+    const f2v sq = xv * xv;
+    return (sq.x + sq.y) * a.norm;
   }
   // stores bin k's power; returns the value the spectrum holds (fp16-rounded in P3_POWER16)
   __device__ __forceinline__ float store(uint32_t k, float p) const {
@@ -1228,6 +1230,8 @@ __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Arg
     float2 tk = cmul(rt.t1, w4(static_cast<uint32_t>(t)));  // W_2N^k for k3 = t
     const float2 tk_step = w4(static_cast<uint32_t>(kStreams));
     float2 ta = make_float2(0.f, 0.f), ta_step = make_float2(1.f, 0.f);
+    // (-i)^{n_s}: W_2N^{n_s (M-k)} = (-i)^{n_s} conj(W_2N^{n_s k}) for the mirror bins
+    const float2 rq = rot_mi(make_float2(1.f, 0.f), n_s);
     if (correct) {
       ta = cmul(rt.ta, w4((n_s * static_cast<uint32_t>(t)) % L4));
       ta_step = w4((n_s * static_cast<uint32_t>(kStreams)) % L4);
@@ -1247,10 +1251,9 @@ __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Arg
       emit(k, untangle_w(zk, zm, w), tk, ta);
       if (c != 0 && c != half) {
         const uint32_t kk = a.M - k;                 // = cm + C*(L-1-k3)
-        const float2 wm = make_float2(-w.x, w.y);  // W_N^{M-k} = -conj(W_N^k)
-        const float2 tkm = make_float2(-tk.y, -tk.x);
-        const float2 tam = rot_mi(conjf2(ta), n_s);
-        emit(kk, untangle_w(zm, zk, wm), tkm, tam);
+        const float2 tkm = make_float2(-tk.y, -tk.x);  // W_2N^{M-k} = -i conj(W_2N^k)
+        const float2 tam = cmulc(rq, ta);
+        emit(kk, untangle_wm(zm, zk, w), tkm, tam);
       }
       if (c == 0 && k3 == 0) emit.nyquist(zk, n_s);
     }

@@ -38,15 +38,44 @@ struct TwiddleTable {
 };
 
 #if defined(__HIP__)
+// Complex arithmetic as packed-FP32 vector operations (v_pk_add_f32,
+// v_pk_mul_f32, v_pk_fma_f32). Written on a native 2-float vector, the
+// element broadcasts, swaps and sign changes fold into the instructions'
+// op_sel / neg modifiers or into a scalar-register sign pair; written per
+// component (make_float2(a.x * b.x - a.y * b.y, ...)) the compiler paired
+// the operands with register moves and sign flips with v_xor: a complex
+// product took ~4.5 VALU instead of 2, a radix-4 butterfly ~1.5x its packed
+// count (tools/isa_mix.py, round 5).
+using f2v = float __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2v vec(float2 a) { return f2v{a.x, a.y}; }
+__device__ __forceinline__ float2 unvec(f2v a) { return make_float2(a.x, a.y); }
+// a * b: a.x * (b.x, b.y) + a.y * (-b.y, b.x), one v_pk_mul_f32 + one v_pk_fma_f32
 __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
-  return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+  const f2v av = vec(a), bv = vec(b);
+  const f2v bs = {-bv.y, bv.x};
+  return unvec(av.xx * bv + av.yy * bs);
 }
-__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
-__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return unvec(vec(a) + vec(b)); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return unvec(vec(a) - vec(b)); }
 __device__ __forceinline__ float2 conjf2(float2 a) { return make_float2(a.x, -a.y); }
 // multiply by -i (forward-transform rotation)
 __device__ __forceinline__ float2 mul_mi(float2 a) { return make_float2(a.y, -a.x); }
-__device__ __forceinline__ float2 cscale(float2 a, float s) { return make_float2(a.x * s, a.y * s); }
+__device__ __forceinline__ float2 cscale(float2 a, float s) { return unvec(vec(a) * s); }
+// a + s (-i) d = (a.x + s d.y, a.y - s d.x) and a - s (-i) d, one v_pk_fma_f32
+// each (the swap in op_sel, the signs in a scalar pair; s = 1 is exact: one
+// rounding, the same value as the add)
+__device__ __forceinline__ float2 add_mi(float2 a, float2 d, float s = 1.0f) {
+  const f2v sg = {s, -s};
+  return unvec(__builtin_elementwise_fma(vec(d).yx, sg, vec(a)));
+}
+__device__ __forceinline__ float2 sub_mi(float2 a, float2 d, float s = 1.0f) {
+  const f2v sg = {-s, s};
+  return unvec(__builtin_elementwise_fma(vec(d).yx, sg, vec(a)));
+}
+// a + s b (one v_pk_fma_f32)
+__device__ __forceinline__ float2 cfma(float s, float2 b, float2 a) {
+  return unvec(__builtin_elementwise_fma(f2v{s, s}, vec(b), vec(a)));
+}
 
 // j mod m (m < 2^32, j < 2^60) from a double-precision quotient estimate,
 // corrected exactly: gfx950 has no 64-bit integer divide, and the compiler's
