@@ -409,7 +409,7 @@ __device__ __forceinline__ double block_sum(double v, double* scratch) {
 __device__ __forceinline__ float2 cmulc(float2 a, float2 b) {
   const f2v av = vec(a), bv = vec(b);
   const f2v bc = {bv.x, -bv.y};
-  return unvec(av.xx * bc + av.yy * bv.yx);
+  return unvec(__builtin_elementwise_fma(av.yy, bv.yx, av.xx * bc));  // as cmul
 }
 
 // X_k of the real FFT from Z_k, Z_{M-k} of the packed complex FFT and w = W_N^k:
