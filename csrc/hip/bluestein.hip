@@ -70,17 +70,31 @@ __device__ __forceinline__ float2 bs_bin(const float2* A, uint32_t Mb, uint32_t 
   return untangle_w(zk, zm, tw_lookup(tw, 2ull * k));  // W_N^k = W_2N^{2k}
 }
 
-// Each thread handles kPowBins consecutive bins k: W_2N^k and W_2N^{n_s k}
+// Each thread handles kPowBins bins k (kThreads apart): W_2N^k and W_2N^{n_s k}
 // (the padding correction) are looked up exactly for the first and stepped by
 // one complex product per bin after it (one 64-bit reduction and table pair
 // per kPowBins bins instead of two per bin: n_s k mod 2N lands anywhere in the
-// table). Stores of the bins are contiguous per thread.
-constexpr int kPowBins = 4;
+// table). A wave's loads and stores cover 64 consecutive bins.
+// Measured (one call, templates/s at -P 2.7 / 2.9 / 1.1): 4 contiguous bins
+// 3 719 / 3 756 / 9 804, 8 contiguous 3 518 / 3 164 / 9 212, 4 strided
+// 3 810 / 3 956 / 10 149, 8 strided 3 865 / 3 980 / 10 171 (default)
+#ifndef BRP_POW_BINS
+#define BRP_POW_BINS 8
+#endif
+#ifndef BRP_POW_STRIDED
+#define BRP_POW_STRIDED 1
+#endif
+constexpr int kPowBins = BRP_POW_BINS;
+// strided form: the thread's bins are kThreads apart (every load and store
+// instruction of a wave covers 64 consecutive bins)
+constexpr bool kPowStrided = BRP_POW_STRIDED != 0;
+constexpr uint32_t kPowStep = kPowStrided ? kThreads : 1;
 
 template <bool HALF>
 __global__ void __launch_bounds__(kThreads) bs_power_kernel(BsPowerArgs a) {
   const int b = blockIdx.y;  // transform
-  const uint32_t k0 = (blockIdx.x * kThreads + threadIdx.x) * kPowBins;
+  const uint32_t k0 = kPowStrided ? blockIdx.x * kThreads * kPowBins + threadIdx.x
+                                  : (blockIdx.x * kThreads + threadIdx.x) * kPowBins;
   if (k0 >= a.limit) return;
   const uint32_t real_bins = a.nsamples / 2 + 1;  // bins the real DFT defines
   const float2* A = a.A + static_cast<size_t>(b) * a.L;
@@ -96,9 +110,9 @@ __global__ void __launch_bounds__(kThreads) bs_power_kernel(BsPowerArgs a) {
     if (w.n_s > 0) {
       w.dS = static_cast<float>(a.delta[t]);
       w.tk = tw_lookup(a.tw, k0);
-      w.sk = tw_lookup(a.tw, 1);
+      w.sk = tw_lookup(a.tw, kPowStep);
       w.ta = tw_lookup(a.tw, static_cast<uint64_t>(w.n_s) * k0);
-      w.sa = tw_lookup(a.tw, w.n_s);
+      w.sa = tw_lookup(a.tw, static_cast<uint64_t>(w.n_s) * kPowStep);
     }
     return w;
   };
@@ -125,7 +139,7 @@ __global__ void __launch_bounds__(kThreads) bs_power_kernel(BsPowerArgs a) {
     Walk w = walk(b);
 #pragma unroll
     for (int i = 0; i < kPowBins; ++i) {
-      const uint32_t k = k0 + i;
+      const uint32_t k = k0 + i * kPowStep;
       if (k >= a.limit) break;
       const bool live = k > 0 && k < real_bins;
       store(b, k, live ? power(bs_bin(A, a.Mb, a.nsamples, a.tw, k), w) : 0.0f);
@@ -139,7 +153,7 @@ __global__ void __launch_bounds__(kThreads) bs_power_kernel(BsPowerArgs a) {
   Walk wa = walk(ta), wb = has_b ? walk(tb) : Walk{};
 #pragma unroll
   for (int i = 0; i < kPowBins; ++i) {
-    const uint32_t k = k0 + i;
+    const uint32_t k = k0 + i * kPowStep;
     if (k >= a.limit) break;
     const bool live = k > 0 && k < real_bins;
     float pa = 0.0f, pb = 0.0f;
