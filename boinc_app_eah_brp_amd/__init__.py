@@ -36,15 +36,21 @@ def native():
             import torch  # noqa: F401
         except Exception:  # pragma: no cover - torch is optional for CPU-only use
             pass
+    # BRP_CHECKED=1: the device-side debug build (csrc/hip/checked.hpp)
+    checked = os.environ.get("BRP_CHECKED", "0") not in ("", "0")
+    name = "._brp_checked" if checked else "._brp"
     try:
-        _native = importlib.import_module("._brp", __name__)
+        _native = importlib.import_module(name, __name__)
     except ImportError:
         if os.environ.get("BRP_NO_AUTOBUILD"):
             raise
         from . import _build
 
-        _build.build(verbose=False)
-        _native = importlib.import_module("._brp", __name__)
+        if checked:
+            _build.build_checked(verbose=False)
+        else:
+            _build.build(verbose=False)
+        _native = importlib.import_module(name, __name__)
     return _native
 
 

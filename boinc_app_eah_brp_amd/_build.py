@@ -4,6 +4,10 @@ Products (all git-ignored, shipped to GPU boxes with the repo snapshot):
   boinc_app_eah_brp_amd/_brp<EXT_SUFFIX>   Python extension (pybind11)
   bin/einsteinbinary_mi355x                BOINC application (C++ main)
   build/obj/*.o                            object cache
+  --checked: boinc_app_eah_brp_amd/_brp_checked<EXT_SUFFIX> and
+  bin/einsteinbinary_mi355x_checked, the device-side debug build
+  (csrc/hip/checked.hpp: serialised, verified launches and bounds-checked
+  kernel accesses; BRP_CHECKED=1 makes the package load it)
 
 Device code is compiled for gfx950 only with hipcc; host-only C++ with
 amdclang++. Run:  python -m boinc_app_eah_brp_amd._build [--force] [-j N]
@@ -32,11 +36,12 @@ HOST_SRCS = [
     "core/log.cpp", "core/io.cpp", "core/stats.cpp", "core/gsl_compat.cpp", "core/rngmed.cpp",
     "core/search_core.cpp", "core/cpu_fft.cpp", "core/cpu_backend.cpp", "core/wisdom.cpp", "core/trace.cpp",
     "boinc/runtime.cpp", "boinc/crash.cpp", "boinc/ipc.cpp",
-    "engine/cpu_engine.cpp", "engine/hip_engine.cpp",
+    "engine/cpu_engine.cpp", "engine/hip_engine.cpp", "engine/checked.cpp",
     "app/search.cpp", "app/multi.cpp", "app/passes.cpp", "app/cli.cpp",
 ]
 DEVICE_SRCS = [
     "hip/fft_passes.hip", "hip/bluestein.hip", "hip/harmonic_sum.hip", "hip/resample.hip", "hip/whiten.hip", "hip/rmed_wide.hip",
+    "hip/checked.hip",
 ]
 BINDING_SRCS = ["bindings/pybind.cpp"]
 APP_MAIN = "app/main.cpp"
@@ -90,23 +95,38 @@ def asan_app_path() -> Path:
     return BIN / "einsteinbinary_mi355x_asan"
 
 
-def _compile(src_rel: str, force: bool, hdr_mtime: float, sanitize: bool = False) -> tuple[str, Path]:
+OBJ_CHECKED = ROOT / "build" / "obj_checked"
+
+
+def checked_extension_path() -> Path:
+    return PKG / f"_brp_checked{ext_suffix()}"
+
+
+def checked_app_path() -> Path:
+    return BIN / "einsteinbinary_mi355x_checked"
+
+
+def _compile(src_rel: str, force: bool, hdr_mtime: float, sanitize: bool = False,
+             checked: bool = False) -> tuple[str, Path]:
     src = CSRC / src_rel
-    obj = (OBJ_SAN if sanitize else OBJ) / (src_rel.replace("/", "__") + ".o")
+    obj = (OBJ_SAN if sanitize else OBJ_CHECKED if checked else OBJ) / (src_rel.replace("/", "__") + ".o")
     if not _needs(obj, src, hdr_mtime, force):
         return "cached", obj
     obj.parent.mkdir(parents=True, exist_ok=True)
     san_host = [f for s in SAN for f in ("-Xarch_host", f"-fsanitize={s}")] if sanitize else []
     san_cxx = [f"-fsanitize={s}" for s in SAN] + ["-fno-omit-frame-pointer", "-g"] if sanitize else []
+    chk = ["-DBRP_CHECKED=1"] if checked else []
     if src.suffix == ".hip":
-        cmd = [HIPCC, f"--offload-arch={ARCH}", *_common_flags(), "-munsafe-fp-atomics", *san_host,
+        cmd = [HIPCC, f"--offload-arch={ARCH}", *_common_flags(), *chk, "-munsafe-fp-atomics", *san_host,
                *(["-Xarch_host", "-fno-omit-frame-pointer"] if sanitize else []), "-c", str(src), "-o", str(obj)]
     else:
-        flags = _common_flags() + san_cxx
+        flags = _common_flags() + chk + san_cxx
         if src_rel.startswith("bindings/"):
             import pybind11
             flags += [f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}",
                       "-fvisibility=hidden"]
+            if checked:
+                flags += ["-DBRP_MODULE_NAME=_brp_checked"]
         cmd = [CLANG, *flags, "-c", str(src), "-o", str(obj)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
@@ -181,15 +201,49 @@ def build_asan(force: bool = False, jobs: int | None = None, verbose: bool = Tru
     return app
 
 
+def build_checked(force: bool = False, jobs: int | None = None, verbose: bool = True) -> dict:
+    """Device-side debug build (csrc/hip/checked.hpp): module _brp_checked and
+    bin/einsteinbinary_mi355x_checked."""
+    jobs = jobs or min(16, os.cpu_count() or 4)
+    hdr = _headers_mtime()
+    srcs = HOST_SRCS + DEVICE_SRCS + BINDING_SRCS + [APP_MAIN]
+    results = {}
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        futs = {ex.submit(_compile, s, force, hdr, False, True): s for s in srcs}
+        for f in cf.as_completed(futs):
+            status, obj = f.result()
+            results[futs[f]] = obj
+            if verbose and status == "built":
+                print(f"[build checked] {futs[f]}", flush=True)
+    core = [results[s] for s in HOST_SRCS + DEVICE_SRCS]
+    ext = checked_extension_path()
+    ext_objs = core + [results[s] for s in BINDING_SRCS]
+    if force or not ext.exists() or ext.stat().st_mtime < max(o.stat().st_mtime for o in ext_objs):
+        _link(ext_objs, ext, shared=True)
+        if verbose:
+            print(f"[build checked] linked {ext.relative_to(ROOT)}", flush=True)
+    app = checked_app_path()
+    app_objs = core + [results[APP_MAIN]]
+    if force or not app.exists() or app.stat().st_mtime < max(o.stat().st_mtime for o in app_objs):
+        _link(app_objs, app, shared=False)
+        if verbose:
+            print(f"[build checked] linked {app.relative_to(ROOT)}", flush=True)
+    return {"checked_extension": str(ext), "checked_app": str(app)}
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", "--jobs", type=int, default=None)
     ap.add_argument("--asan", action="store_true", help="also build bin/einsteinbinary_mi355x_asan (ASan + UBSan)")
+    ap.add_argument("--checked", action="store_true",
+                    help="also build the device-side debug build (_brp_checked, bin/einsteinbinary_mi355x_checked)")
     a = ap.parse_args(argv)
     out = build(force=a.force, jobs=a.jobs)
     if a.asan:
         out["asan_app"] = str(build_asan(force=a.force, jobs=a.jobs))
+    if a.checked:
+        out.update(build_checked(force=a.force, jobs=a.jobs))
     print(out)
     return 0
 

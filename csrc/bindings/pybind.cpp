@@ -23,6 +23,7 @@
 #include "../core/stats.hpp"
 #include "../core/wisdom.hpp"
 #include "../engine/hip_engine.hpp"
+#include "../hip/checked.hpp"
 
 namespace py = pybind11;
 using namespace brp;
@@ -193,7 +194,11 @@ std::vector<TemplateInput> arrays_to_templates(py::array_t<float> P, py::array_t
 
 }  // namespace
 
-PYBIND11_MODULE(_brp, m) {
+// the checked build (_build.py --checked) is the module _brp_checked
+#ifndef BRP_MODULE_NAME
+#define BRP_MODULE_NAME _brp
+#endif
+PYBIND11_MODULE(BRP_MODULE_NAME, m) {
   m.doc() = "MI355X-native Einstein@Home binary radio pulsar search: native core";
   m.attr("DD_HEADER_SIZE") = sizeof(DDHeader);
   m.attr("CP_HEADER_SIZE") = sizeof(CPHeader);
@@ -271,6 +276,21 @@ PYBIND11_MODULE(_brp, m) {
       .def("get", &Taus2::get)
       .def("uniform", &Taus2::uniform);
   m.def("gaussian_ziggurat", &gaussian_ziggurat);
+  m.def("checked_build", &hipk::checked_build,
+        "True in the device-side debug build (_brp_checked: bounds-checked kernel accesses, verified launches)");
+  m.def(
+      "device_check",
+      []() {
+        std::string rep;
+        int rc;
+        {
+          py::gil_scoped_release rel;
+          rc = hipk::device_check(&rep);
+        }
+        if (rc) throw std::runtime_error(rep);
+      },
+      "Synchronise the device and raise RuntimeError naming the fault if any work since the last check failed "
+      "(checked build: the kernel, source line and address of an out-of-bounds access or guard-zone write)");
   m.def("hip_running_median", [](py::array_t<float, py::array::c_style> x, uint32_t w, int reps, int device) {
     std::vector<float> in(x.data(), x.data() + x.size()), out;
     double ms = 0;

@@ -71,15 +71,17 @@ bool make_bluestein_plan(uint32_t Mb, FFTPlan3& plan) {
   if (lens.empty()) return false;
   std::sort(lens.begin(), lens.end());
   lens.erase(std::unique(lens.begin(), lens.end()), lens.end());
-  // the smallest length whose plan runs the transposed convolution
-  // (hipk::chirp_rev_supported), unless that costs more than 3 % in length
   // BRP_BS_PLAN=L1xL2xL3 (A/B): that factorisation when it covers the length
+  // and meets the enumeration's constraints (L2 <= L1, the pass-2 twiddle
+  // table's L2 L3 <= kMaxL2L3, a length below 2^31); otherwise ignored
   if (const char* e = std::getenv("BRP_BS_PLAN")) {
     unsigned a1 = 0, a2 = 0, a3 = 0;
-    if (std::sscanf(e, "%ux%ux%u", &a1, &a2, &a3) == 3 && static_cast<uint64_t>(a1) * a2 * a3 >= need &&
+    const bool parsed = std::sscanf(e, "%ux%ux%u", &a1, &a2, &a3) == 3;
+    const uint64_t len = static_cast<uint64_t>(a1) * a2 * a3;
+    if (parsed && len >= need && len < (1ull << 31) && a2 <= a1 && static_cast<uint64_t>(a2) * a3 <= kMaxL2L3 &&
         hipk::pass12_length_supported(a1) && hipk::pass12_length_supported(a2) && hipk::pass3_length_supported(a3)) {
       plan = FFTPlan3();
-      plan.M = a1 * a2 * a3;
+      plan.M = static_cast<uint32_t>(len);
       plan.L1 = a1;
       plan.L2 = a2;
       plan.L3 = a3;
@@ -87,6 +89,8 @@ bool make_bluestein_plan(uint32_t Mb, FFTPlan3& plan) {
       plan.rows3 = 8;
       return true;
     }
+    log_message(LOG_WARN, true, "BRP_BS_PLAN=%s ignored: not a supported factorisation of a length >= %llu.\n", e,
+                static_cast<unsigned long long>(need));
   }
   if (want_l3) {
     for (uint64_t L : lens)
@@ -167,24 +171,33 @@ struct DevBuf {
   size_t n = 0;
   // fine: fine-grained device memory the host can read and write in place
   // (over the PCIe BAR) -- used for the per-batch parameters and results
+  // checked build (hipk::checked_build()): a guard zone behind the requested
+  // bytes, and the allocation in the registry the device-side checks read
   int alloc(size_t count, bool fine = false) {
     release();
     if (count == 0) return 0;
-    const hipError_t e = fine ? hipExtMallocWithFlags(reinterpret_cast<void**>(&p), count * sizeof(T),
-                                                      hipDeviceMallocFinegrained)
-                              : hipMalloc(&p, count * sizeof(T));
+    const size_t bytes = count * sizeof(T), total = bytes + hipk::chk_guard_bytes();
+    const hipError_t e = fine ? hipExtMallocWithFlags(reinterpret_cast<void**>(&p), total, hipDeviceMallocFinegrained)
+                              : hipMalloc(&p, total);
     if (fault_device_alloc() || e != hipSuccess) {
       if (e == hipSuccess) (void)hipFree(p);  // injected failure
       else (void)hipGetLastError();
       p = nullptr;
-      log_message(LOG_ERROR, true, "Couldn't allocate %zu bytes of device memory!\n", count * sizeof(T));
+      log_message(LOG_ERROR, true, "Couldn't allocate %zu bytes of device memory!\n", bytes);
       return RADPUL_HIP_MEM_ALLOC_DEVICE;
+    }
+    if (total > bytes) {
+      if (hipk::chk_fill_guard(p, bytes) != hipSuccess) (void)hipGetLastError();
+      hipk::chk_register(p, bytes, total);
     }
     n = count;
     return 0;
   }
   void release() {
-    if (p) (void)hipFree(p);
+    if (p) {
+      hipk::chk_unregister(p);
+      (void)hipFree(p);
+    }
     p = nullptr;
     n = 0;
   }
@@ -224,14 +237,25 @@ struct PinnedBuf {
     n = 0;
     pageable = false;
   }
+  // at least `count` elements (contents not kept)
+  int reserve(size_t count) { return count <= n ? 0 : alloc(count); }
   ~PinnedBuf() { release(); }
 };
 
 // Synchronous copy on the engine's own stream. A plain hipMemcpy goes through
 // the null stream, whose first use creates one more hardware queue: 7.5-8.3 ms
 // of start-up on MI355X (tools/experiments/startup/, profiles/README.md round 3).
+// Every host <-> device copy of the engine: the host side is pinned memory
+// (or a host view of fine-grained device memory), never pageable memory; the
+// checked build verifies that (hipk::chk_host_copy).
+hipError_t memcpy_async(void* dst, const void* src, size_t bytes, hipMemcpyKind kind, hipStream_t s) {
+  if (kind == hipMemcpyHostToDevice) hipk::chk_host_copy(src, bytes);
+  else if (kind == hipMemcpyDeviceToHost) hipk::chk_host_copy(dst, bytes);
+  return hipMemcpyAsync(dst, src, bytes, kind, s);
+}
+
 hipError_t copy_sync(void* dst, const void* src, size_t bytes, hipMemcpyKind kind, hipStream_t s) {
-  const hipError_t e = hipMemcpyAsync(dst, src, bytes, kind, s);
+  const hipError_t e = memcpy_async(dst, src, bytes, kind, s);
   if (e != hipSuccess) return e;
   return hipStreamSynchronize(s);
 }
@@ -249,12 +273,13 @@ void* host_view(int device, void* p, size_t bytes, hipStream_t s) {
   log_message(LOG_DEBUG, true, "fine-grained buffer %p: large BAR %d, host pointer %p -> %p\n", p, large_bar,
               at.hostPointer, h);
   if (!large_bar) return nullptr;
-  std::vector<uint8_t> pat(bytes), back(bytes);
+  std::vector<uint8_t> pat(bytes);
   for (size_t i = 0; i < bytes; ++i) pat[i] = static_cast<uint8_t>(i * 37u + 11u);
   std::memcpy(h, pat.data(), bytes);
   std::atomic_thread_fence(std::memory_order_seq_cst);
-  if (copy_sync(back.data(), p, bytes, hipMemcpyDeviceToHost, s) != hipSuccess) return nullptr;
-  return pat == back ? h : nullptr;
+  PinnedBuf<uint8_t> back;
+  if (back.alloc(bytes) || copy_sync(back.p, p, bytes, hipMemcpyDeviceToHost, s) != hipSuccess) return nullptr;
+  return std::memcmp(pat.data(), back.p, bytes) == 0 ? h : nullptr;
 }
 
 // W_{2N}^j = exp(-i pi j / N) as a two-level float table
@@ -519,8 +544,42 @@ struct HipEngine::Impl {
   // the pipelines that read the series order themselves after it with
   // ev_w1 (adopt_series), so the host's prepare / launch work overlaps the
   // whitening kernels. The host noise arrays stay alive until ev_w1 has passed.
-  std::vector<float2> w_zn_host;
-  std::vector<uint32_t> w_zb_host;
+  PinnedBuf<uint32_t> w_zb_host;  // pinned: the copies are truly asynchronous
+  PinnedBuf<float2> w_zn_host;
+  // Host copies of the engine go through its own pinned buffers, never through
+  // the runtime's pageable-memory path (which pins the caller's pages for each
+  // copy and has the device write them: the one device fault seen on a test
+  // box, round 5, was such a copy; profiles/fault_r6.txt): `stage` bounces the
+  // large one-off copies (series, spectra, cells, tables) in chunks, `list_host`
+  // receives candidate lists too long to read in place.
+  PinnedBuf<uint8_t> stage;
+  PinnedBuf<uint2> list_host;
+  static constexpr size_t kStageChunk = 8u << 20;
+  hipError_t copy_out(void* dst, const void* src, size_t bytes) {
+    if (bytes == 0) return hipSuccess;
+    if (stage.reserve(std::min(bytes, kStageChunk))) return hipErrorOutOfMemory;
+    for (size_t off = 0; off < bytes; off += kStageChunk) {
+      const size_t nb = std::min(kStageChunk, bytes - off);
+      hipError_t e = memcpy_async(stage.p, static_cast<const uint8_t*>(src) + off, nb, hipMemcpyDeviceToHost, stream);
+      if (e == hipSuccess) e = hipStreamSynchronize(stream);
+      if (e != hipSuccess) return e;
+      std::memcpy(static_cast<uint8_t*>(dst) + off, stage.p, nb);
+    }
+    return hipSuccess;
+  }
+  hipError_t copy_in(void* dst, const void* src, size_t bytes) {
+    if (bytes == 0) return hipSuccess;
+    if (stage.reserve(std::min(bytes, kStageChunk))) return hipErrorOutOfMemory;
+    for (size_t off = 0; off < bytes; off += kStageChunk) {
+      const size_t nb = std::min(kStageChunk, bytes - off);
+      hipError_t e = hipStreamSynchronize(stream);  // the stage's previous chunk has been read
+      if (e != hipSuccess) return e;
+      std::memcpy(stage.p, static_cast<const uint8_t*>(src) + off, nb);
+      e = memcpy_async(static_cast<uint8_t*>(dst) + off, stage.p, nb, hipMemcpyHostToDevice, stream);
+      if (e != hipSuccess) return e;
+    }
+    return hipStreamSynchronize(stream);
+  }
   hipEvent_t ev_w0 = nullptr, ev_w1 = nullptr, ev_adopt = nullptr;
   bool w_pending = false;       // ev_w0 / ev_w1 of an asynchronous whitening not yet accounted
   // whitening device time of a finished asynchronous whitening into the stats
@@ -563,8 +622,7 @@ struct HipEngine::Impl {
   int upload(DevBuf<float2>& d, const std::vector<float2>& h) {
     int rc = d.alloc(h.size());
     if (rc) return rc;
-    if (copy_sync(d.p, h.data(), h.size() * sizeof(float2), hipMemcpyHostToDevice, stream) != hipSuccess)
-      return RADPUL_HIP_MEM_COPY_HOST_DEVICE;
+    if (copy_in(d.p, h.data(), h.size() * sizeof(float2)) != hipSuccess) return RADPUL_HIP_MEM_COPY_HOST_DEVICE;
     return 0;
   }
 
@@ -849,7 +907,7 @@ struct HipEngine::Impl {
         // n_steps comes with the parameters (host bracketed search); pass 1
         // zeroes the batch's candidate counter
         if (fg_in) return hipSuccess;  // the host wrote `in` directly
-        return hipMemcpyAsync(in.p, h_in.p, thr_bytes + sizeof(TemplateDev) * nb, hipMemcpyHostToDevice, stream);
+        return memcpy_async(in.p, h_in.p, thr_bytes + sizeof(TemplateDev) * nb, hipMemcpyHostToDevice, stream);
       case kPass1:
         if (bs) return bs_template_in(nb, group_reset ? &cands.p[0].x : nullptr);
         return fft_pass1(nb, group_reset ? &cands.p[0].x : nullptr);
@@ -900,7 +958,7 @@ struct HipEngine::Impl {
       }
       case kEpilogue:
         if (fg_out) return hipSuccess;  // the host reads `cands` directly
-        return hipMemcpyAsync(h_cands.p, cands.p, sizeof(uint2) * (1 + kcopy), hipMemcpyDeviceToHost, stream);
+        return memcpy_async(h_cands.p, cands.p, sizeof(uint2) * (1 + kcopy), hipMemcpyDeviceToHost, stream);
       default: return hipErrorInvalidValue;
     }
   }
@@ -1011,7 +1069,11 @@ int hip_running_median(int device, const std::vector<float>& in, uint32_t W, std
     return wide ? hipk::launch_running_median_wide(din.p, n_in, W, dout.p, scratch.p, nullptr)
                 : hipk::launch_running_median(din.p, n_in, W, dout.p, nullptr);
   };
-  BRP_HIP_CHECK(hipMemcpy(din.p, in.data(), in.size() * sizeof(float), hipMemcpyHostToDevice),
+  // pinned bounce buffer (no runtime pageable-copy path, see Impl::copy_out)
+  PinnedBuf<float> hbuf;
+  if ((rc = hbuf.alloc(std::max(in.size(), n_out)))) return rc;
+  std::memcpy(hbuf.p, in.data(), in.size() * sizeof(float));
+  BRP_HIP_CHECK(hipMemcpy(din.p, hbuf.p, in.size() * sizeof(float), hipMemcpyHostToDevice),
                 RADPUL_HIP_MEM_COPY_HOST_DEVICE);
   hipEvent_t e0, e1;
   BRP_HIP_CHECK(hipEventCreate(&e0), RADPUL_HIP_DEVICE_SET);
@@ -1027,8 +1089,9 @@ int hip_running_median(int device, const std::vector<float>& in, uint32_t W, std
   (void)hipEventDestroy(e1);
   if (ms_per_call) *ms_per_call = reps > 0 ? ms / reps : 0.0;
   out.resize(n_out);
-  BRP_HIP_CHECK(hipMemcpy(out.data(), dout.p, n_out * sizeof(float), hipMemcpyDeviceToHost),
+  BRP_HIP_CHECK(hipMemcpy(hbuf.p, dout.p, n_out * sizeof(float), hipMemcpyDeviceToHost),
                 RADPUL_HIP_MEM_COPY_DEVICE_HOST);
+  std::memcpy(out.data(), hbuf.p, n_out * sizeof(float));
   return 0;
 }
 
@@ -1119,8 +1182,7 @@ int HipEngine::upload_series0(const float* host, const float* dev_src, int src_d
     const size_t nb = packed->packed.size();
     int rc;
     if (d.wu_packed.n < nb && (rc = d.wu_packed.alloc(nb))) return rc;
-    BRP_HIP_CHECK(hipMemcpyAsync(d.wu_packed.p, packed->packed.data(), nb, hipMemcpyHostToDevice, d.stream),
-                  RADPUL_HIP_MEM_COPY_HOST_DEVICE);
+    BRP_HIP_CHECK(d.copy_in(d.wu_packed.p, packed->packed.data(), nb), RADPUL_HIP_MEM_COPY_HOST_DEVICE);
     BRP_HIP_CHECK(hipk::launch_unpack(d.wu_packed.p, static_cast<uint32_t>(nb), packed->four_bit, packed->header.scale,
                                       d.series.p, d.g.n_unpadded, d.stream),
                   RADPUL_HIP_KERNEL_INVOKE);
@@ -1136,7 +1198,7 @@ int HipEngine::upload_series0(const float* host, const float* dev_src, int src_d
     return 0;
   }
   trace::Range up("brp:series_upload");
-  BRP_HIP_CHECK(copy_sync(d.series.p, host, bytes, hipMemcpyHostToDevice, d.stream), RADPUL_HIP_MEM_COPY_HOST_DEVICE);
+  BRP_HIP_CHECK(d.copy_in(d.series.p, host, bytes), RADPUL_HIP_MEM_COPY_HOST_DEVICE);
   return 0;
 }
 
@@ -1304,10 +1366,8 @@ int HipEngine::setup_impl(const SearchGeometry& g, const float* host_series, con
   const std::vector<float2>& lo = twc.second;
   if ((rc = d.tw_hi.alloc(hi.size()))) return rc;
   if ((rc = d.tw_lo.alloc(lo.size()))) return rc;
-  BRP_HIP_CHECK(copy_sync(d.tw_hi.p, hi.data(), hi.size() * sizeof(float2), hipMemcpyHostToDevice, d.stream),
-                RADPUL_HIP_MEM_COPY_HOST_DEVICE);
-  BRP_HIP_CHECK(copy_sync(d.tw_lo.p, lo.data(), lo.size() * sizeof(float2), hipMemcpyHostToDevice, d.stream),
-                RADPUL_HIP_MEM_COPY_HOST_DEVICE);
+  BRP_HIP_CHECK(d.copy_in(d.tw_hi.p, hi.data(), hi.size() * sizeof(float2)), RADPUL_HIP_MEM_COPY_HOST_DEVICE);
+  BRP_HIP_CHECK(d.copy_in(d.tw_lo.p, lo.data(), lo.size() * sizeof(float2)), RADPUL_HIP_MEM_COPY_HOST_DEVICE);
   if ((rc = d.build_tables())) return rc;
   if (d.bs) {
     BRP_HIP_CHECK(d.bs_make_h(), RADPUL_HIP_KERNEL_INVOKE);
@@ -1388,8 +1448,8 @@ int HipEngine::load_slot(uint32_t k, const std::vector<float>& series, float mu0
   BRP_HIP_CHECK(hipSetDevice(d.device), RADPUL_HIP_DEVICE_SET);
   d.own_series();
   d.mu0s[k] = mu0;
-  BRP_HIP_CHECK(copy_sync(d.series.p + static_cast<size_t>(k) * d.g.n_unpadded, series.data(),
-                          d.g.n_unpadded * sizeof(float), hipMemcpyHostToDevice, d.stream),
+  BRP_HIP_CHECK(d.copy_in(d.series.p + static_cast<size_t>(k) * d.g.n_unpadded, series.data(),
+                          d.g.n_unpadded * sizeof(float)),
                 RADPUL_HIP_MEM_COPY_HOST_DEVICE);
   return 0;
 }
@@ -1492,10 +1552,8 @@ int HipEngine::whiten(const SearchOptions& opt, const std::vector<ZapRange>& zap
   const uint32_t nz = static_cast<uint32_t>(noise.bin.size());
   // host sources of the async copies must outlive them: engine members,
   // reused only once this whitening's end event has passed (settle_whiten)
-  std::vector<float2>& zn = d.w_zn_host;
-  std::vector<uint32_t>& zb = d.w_zb_host;
-  zn.clear();
-  zb.clear();
+  std::vector<float2> zn;
+  std::vector<uint32_t> zb;
   if (nz) {
     // overlapping zap ranges hit a bin more than once: sequentially the last
     // draw wins, so keep only that one (the device writes bins in parallel)
@@ -1514,9 +1572,12 @@ int HipEngine::whiten(const SearchOptions& opt, const std::vector<ZapRange>& zap
     // kept across passes (a hipFree per pass would synchronise the device)
     if (zbins.n < nzu && (rc = zbins.alloc(nzu))) return rc;
     if (znoise.n < nzu && (rc = znoise.alloc(nzu))) return rc;
-    BRP_HIP_CHECK(hipMemcpyAsync(zbins.p, zb.data(), nzu * sizeof(uint32_t), hipMemcpyHostToDevice, s),
+    if ((rc = d.w_zb_host.reserve(nzu)) || (rc = d.w_zn_host.reserve(nzu))) return rc;
+    std::memcpy(d.w_zb_host.p, zb.data(), nzu * sizeof(uint32_t));
+    std::memcpy(d.w_zn_host.p, zn.data(), nzu * sizeof(float2));
+    BRP_HIP_CHECK(memcpy_async(zbins.p, d.w_zb_host.p, nzu * sizeof(uint32_t), hipMemcpyHostToDevice, s),
                   RADPUL_HIP_MEM_COPY_HOST_DEVICE);
-    BRP_HIP_CHECK(hipMemcpyAsync(znoise.p, zn.data(), nzu * sizeof(float2), hipMemcpyHostToDevice, s),
+    BRP_HIP_CHECK(memcpy_async(znoise.p, d.w_zn_host.p, nzu * sizeof(float2), hipMemcpyHostToDevice, s),
                   RADPUL_HIP_MEM_COPY_HOST_DEVICE);
     BRP_HIP_CHECK(hipk::launch_zap(spec.p, fft_size, zbins.p, znoise.p, nzu, s), RADPUL_HIP_KERNEL_INVOKE);
   }
@@ -1569,12 +1630,11 @@ int HipEngine::whiten(const SearchOptions& opt, const std::vector<ZapRange>& zap
   }
   d.mu0s[slot] = 0.0f;  // whitened series has its DC (and first window_2 bins) removed
   if (copy_back) {
-    BRP_HIP_CHECK(hipMemcpyAsync(series.data(), slot_series, g.n_unpadded * sizeof(float), hipMemcpyDeviceToHost, s),
-                  RADPUL_HIP_MEM_COPY_DEVICE_HOST);
     {
       trace::Range wait("brp:whiten_wait");
       BRP_HIP_CHECK(hipStreamSynchronize(s), RADPUL_HIP_KERNEL_INVOKE);
     }
+    BRP_HIP_CHECK(d.copy_out(series.data(), slot_series, g.n_unpadded * sizeof(float)), RADPUL_HIP_MEM_COPY_DEVICE_HOST);
     d.st.whiten_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return 0;
   }
@@ -1728,7 +1788,7 @@ int HipEngine::complete(std::vector<TemplateCands>& out) {
     cnt = o.h_cands_p[0].x;
     d.prev_done = nullptr;  // the statistics chain restarts
   }
-  std::vector<uint2> extra;
+  bool extra = false;  // the list was copied into list_host
   const uint2* src = o.h_cands_p + 1;
   if (cnt > d.cap) {
     // The bounded output itself overflowed: more values >= some template's
@@ -1740,6 +1800,16 @@ int HipEngine::complete(std::vector<TemplateCands>& out) {
     // accepts ends in RADPUL_HIP_CAND_OVERFLOW.
     log_message(LOG_DEBUG, true, "Bounded output overflow (%u > %u slots, %d templates): list of %u slots.\n", cnt,
                 d.cap, nb, cnt);
+    // Every (template, level, bin) is emitted at most once, so a count above
+    // nb x levels x fundamental bins is corrupt. The 32-bit counter cannot wrap
+    // before that: the candidate key holds template << (bin_bits + 3), so
+    // slot_cap x 8 x 2^bin_bits <= 2^32 (hs_key_templates).
+    const uint64_t max_vals = static_cast<uint64_t>(nb) * kNumHarmonicLevels * std::max<uint32_t>(d.g.fundamental_idx_hi, 1);
+    if (cnt > max_vals) {
+      log_message(LOG_ERROR, true, "Bounded output counted %u values, more than the %llu a batch can emit.\n", cnt,
+                  static_cast<unsigned long long>(max_vals));
+      return RADPUL_HIP_CAND_OVERFLOW;
+    }
     DevBuf<uint2> big;
     int rc;
     if ((rc = big.alloc(1 + static_cast<size_t>(cnt)))) return rc;
@@ -1756,15 +1826,18 @@ int HipEngine::complete(std::vector<TemplateCands>& out) {
     d.select_mode = sel0;
     d.select_io(slot);
     BRP_HIP_CHECK(e, RADPUL_HIP_KERNEL_INVOKE);
-    extra.resize(1 + static_cast<size_t>(cnt));
-    BRP_HIP_CHECK(hipMemcpyAsync(extra.data(), big.p, extra.size() * sizeof(uint2), hipMemcpyDeviceToHost, d.stream),
+    if ((rc = d.list_host.reserve(1 + static_cast<size_t>(cnt)))) return rc;
+    BRP_HIP_CHECK(memcpy_async(d.list_host.p, big.p, (1 + static_cast<size_t>(cnt)) * sizeof(uint2), hipMemcpyDeviceToHost,
+                                 d.stream),
                   RADPUL_HIP_MEM_COPY_DEVICE_HOST);
     BRP_HIP_CHECK(hipStreamSynchronize(d.stream), RADPUL_HIP_MEM_COPY_DEVICE_HOST);
-    if (extra[0].x != cnt) {  // the same batch, thresholds and spectrum: cannot differ
-      log_message(LOG_ERROR, true, "Bounded output re-run emitted %u values, the first run %u.\n", extra[0].x, cnt);
+    if (d.list_host.p[0].x != cnt) {  // the same batch, thresholds and spectrum: cannot differ
+      log_message(LOG_ERROR, true, "Bounded output re-run emitted %u values, the first run %u.\n", d.list_host.p[0].x,
+                  cnt);
       return RADPUL_HIP_CAND_OVERFLOW;
     }
-    src = extra.data() + 1;
+    src = d.list_host.p + 1;
+    extra = true;
     d.st.tie_reruns += 1;
     d.st.list_dma_copies += 1;
     d.prev_done = nullptr;
@@ -1778,15 +1851,16 @@ int HipEngine::complete(std::vector<TemplateCands>& out) {
   d.st.candidates += cnt;
   // beyond kcopy entries a DMA copy of the list beats reading it in place
   // (uncached reads over the PCIe BAR) or a second copied prefix
-  if (extra.empty() && cnt > (d.fg_out ? d.inplace_max : d.kcopy)) {
-    extra.resize(cnt);
+  if (!extra && cnt > (d.fg_out ? d.inplace_max : d.kcopy)) {
+    int rc;
+    if ((rc = d.list_host.reserve(cnt))) return rc;
     // stream-ordered (a null-stream copy would invalidate another engine's
     // graph capture running in a sibling thread); waits for a batch queued
     // behind this one too, which writes only its own I/O slot
-    BRP_HIP_CHECK(hipMemcpyAsync(extra.data(), o.cands.p + 1, cnt * sizeof(uint2), hipMemcpyDeviceToHost, d.stream),
+    BRP_HIP_CHECK(memcpy_async(d.list_host.p, o.cands.p + 1, cnt * sizeof(uint2), hipMemcpyDeviceToHost, d.stream),
                   RADPUL_HIP_MEM_COPY_DEVICE_HOST);
     BRP_HIP_CHECK(hipStreamSynchronize(d.stream), RADPUL_HIP_MEM_COPY_DEVICE_HOST);
-    src = extra.data();
+    src = d.list_host.p;
     d.st.list_dma_copies += 1;
   }
   out.clear();
@@ -1809,9 +1883,24 @@ int HipEngine::complete(std::vector<TemplateCands>& out) {
   return 0;
 }
 
+namespace {
+// Test hooks check the whole device before they copy: a fault of earlier work
+// (any stream) is then reported as such, with the checked build's record of
+// the kernel that made it, instead of as a failure of the hook's own copy
+// (round 5: an illegal address surfaced at bound_cells' copy).
+int device_ok(const char* hook) {
+  std::string rep;
+  if (hipk::device_check(&rep) == 0) return 0;
+  log_message(LOG_ERROR, true, "%s: device fault before this call: %s\n", hook, rep.c_str());
+  return RADPUL_HIP_KERNEL_INVOKE;
+}
+}  // namespace
+
 int HipEngine::power_spectrum(const TemplateInput& t, std::vector<float>& ps_out, uint32_t* n_steps) {
   Impl& d = *impl_;
   if (d.io_busy()) return RADPUL_EMISC;
+  BRP_HIP_CHECK(hipSetDevice(d.device), RADPUL_HIP_DEVICE_SET);
+  if (int rc = device_ok("power_spectrum")) return rc;
   d.select_io(0);
   const SearchGeometry& g = d.g;
   TemplateDev td{};
@@ -1821,7 +1910,7 @@ int HipEngine::power_spectrum(const TemplateInput& t, std::vector<float>& ps_out
   d.h_tmpl.p[0] = td;
   hipStream_t s = d.stream;
   if (!d.fg_in)
-    BRP_HIP_CHECK(hipMemcpyAsync(d.tmpl.p, d.h_tmpl.p, sizeof(TemplateDev), hipMemcpyHostToDevice, s),
+    BRP_HIP_CHECK(memcpy_async(d.tmpl.p, d.h_tmpl.p, sizeof(TemplateDev), hipMemcpyHostToDevice, s),
                   RADPUL_HIP_MEM_COPY_HOST_DEVICE);
   std::atomic_thread_fence(std::memory_order_seq_cst);
   if (d.bs) {
@@ -1829,10 +1918,10 @@ int HipEngine::power_spectrum(const TemplateInput& t, std::vector<float>& ps_out
     int rc;
     if ((rc = full.alloc(g.fft_size))) return rc;
     BRP_HIP_CHECK(d.bs_template_spectra(1, full.p, nullptr, g.fft_size, g.fft_size), RADPUL_HIP_KERNEL_INVOKE);
-    ps_out.resize(g.fft_size);
-    BRP_HIP_CHECK(hipMemcpyAsync(ps_out.data(), full.p, g.fft_size * sizeof(float), hipMemcpyDeviceToHost, s),
-                  RADPUL_HIP_MEM_COPY_DEVICE_HOST);
     BRP_HIP_CHECK(hipStreamSynchronize(s), RADPUL_HIP_KERNEL_INVOKE);
+    if (int rc2 = device_ok("power_spectrum")) return rc2;
+    ps_out.resize(g.fft_size);
+    BRP_HIP_CHECK(d.copy_out(ps_out.data(), full.p, g.fft_size * sizeof(float)), RADPUL_HIP_MEM_COPY_DEVICE_HOST);
     if (n_steps) *n_steps = d.h_tmpl.p[0].n_steps;
     return 0;
   }
@@ -1842,10 +1931,10 @@ int HipEngine::power_spectrum(const TemplateInput& t, std::vector<float>& ps_out
   int rc;
   if ((rc = full.alloc(g.fft_size))) return rc;
   BRP_HIP_CHECK(d.fft_pass3(1, full.p, nullptr, g.fft_size, g.fft_size), RADPUL_HIP_KERNEL_INVOKE);
-  ps_out.resize(g.fft_size);
-  BRP_HIP_CHECK(hipMemcpyAsync(ps_out.data(), full.p, g.fft_size * sizeof(float), hipMemcpyDeviceToHost, s),
-                RADPUL_HIP_MEM_COPY_DEVICE_HOST);
   BRP_HIP_CHECK(hipStreamSynchronize(s), RADPUL_HIP_KERNEL_INVOKE);
+  if (int rc2 = device_ok("power_spectrum")) return rc2;
+  ps_out.resize(g.fft_size);
+  BRP_HIP_CHECK(d.copy_out(ps_out.data(), full.p, g.fft_size * sizeof(float)), RADPUL_HIP_MEM_COPY_DEVICE_HOST);
   if (n_steps) *n_steps = d.h_tmpl.p[0].n_steps;
   return 0;
 }
@@ -1854,10 +1943,9 @@ int HipEngine::download_series(std::vector<float>& series) {
   Impl& d = *impl_;
   if (!d.ready || !d.shared_series_valid()) return RADPUL_EMISC;
   BRP_HIP_CHECK(hipSetDevice(d.device), RADPUL_HIP_DEVICE_SET);
-  BRP_HIP_CHECK(hipStreamSynchronize(d.stream), RADPUL_HIP_KERNEL_INVOKE);
+  if (int rc = device_ok("download_series")) return rc;
   series.resize(d.g.n_unpadded);
-  BRP_HIP_CHECK(copy_sync(series.data(), d.series_in(), d.g.n_unpadded * sizeof(float), hipMemcpyDeviceToHost, d.stream),
-                RADPUL_HIP_MEM_COPY_DEVICE_HOST);
+  BRP_HIP_CHECK(d.copy_out(series.data(), d.series_in(), d.g.n_unpadded * sizeof(float)), RADPUL_HIP_MEM_COPY_DEVICE_HOST);
   return 0;
 }
 
@@ -1918,10 +2006,10 @@ int HipEngine::bound_cells(int k, std::vector<float>& cells) {
   Impl& d = *impl_;
   if (!d.ready || k < 0 || k >= d.batch || !d.hs_prune || d.hs_cell_shift != 3) return RADPUL_EVAL;
   BRP_HIP_CHECK(hipSetDevice(d.device), RADPUL_HIP_DEVICE_SET);
-  BRP_HIP_CHECK(hipStreamSynchronize(d.stream), RADPUL_HIP_KERNEL_INVOKE);
+  if (int rc = device_ok("bound_cells")) return rc;
   cells.resize((d.ps_stride >> 3) + 8);
-  BRP_HIP_CHECK(copy_sync(cells.data(), d.pyr.p + static_cast<size_t>(k) * hipk::hs_pyr_stride(d.ps_stride),
-                          cells.size() * sizeof(float), hipMemcpyDeviceToHost, d.stream),
+  BRP_HIP_CHECK(d.copy_out(cells.data(), d.pyr.p + static_cast<size_t>(k) * hipk::hs_pyr_stride(d.ps_stride),
+                           cells.size() * sizeof(float)),
                 RADPUL_HIP_MEM_COPY_DEVICE_HOST);
   return 0;
 }

@@ -34,16 +34,17 @@ __global__ void __launch_bounds__(kThreads) bs_chirp_in_kernel(BsInArgs a) {
     } else if (n < a.Mb) {
       float2 x;
       if (MODE == BS_IN_REAL2) {
-        x = make_float2(2 * n < a.n_real ? a.real_in[2 * n] : 0.0f, 2 * n + 1 < a.n_real ? a.real_in[2 * n + 1] : 0.0f);
+        x = make_float2(2 * n < a.n_real ? BRP_LD(&a.real_in[2 * n]) : 0.0f,
+                       2 * n + 1 < a.n_real ? BRP_LD(&a.real_in[2 * n + 1]) : 0.0f);
       } else if (MODE == BS_IN_REAL1) {
-        x = make_float2(n < a.n_real ? a.real_in[n] : 0.0f, 0.0f);
+        x = make_float2(n < a.n_real ? BRP_LD(&a.real_in[n]) : 0.0f, 0.0f);
       } else if (MODE == BS_IN_CONJ) {
-        x = conjf2(a.cplx_in[n]);
+        x = conjf2(BRP_LD(&a.cplx_in[n]));
       } else {  // BS_IN_HERM_CONJ: F_n = X_n (n <= (N-1)/2), conj(X_{N-n}) above; input conj(F_n)
         // with the whitening's zeroed edges and Im X_0 = 0 (c2r semantics, as tangle_kernel)
         auto bin = [&](uint32_t q) -> float2 {
           if (q < a.w2 || q >= a.fft_size - a.w2) return make_float2(0.0f, 0.0f);
-          float2 v = a.cplx_in[q];
+          float2 v = BRP_LD(&a.cplx_in[q]);
           if (q == 0) v.y = 0.0f;
           return v;
         };
@@ -52,7 +53,7 @@ __global__ void __launch_bounds__(kThreads) bs_chirp_in_kernel(BsInArgs a) {
       }
       v = cmul(x, chirp_w(a.chirp, n));
     }
-    y[n] = v;
+    BRP_ST(&y[n], v);
   }
 }
 
@@ -63,10 +64,13 @@ __global__ void __launch_bounds__(kThreads) bs_chirp_in_kernel(BsInArgs a) {
 __device__ __forceinline__ float2 bs_bin(const float2* A, uint32_t Mb, uint32_t N, const TwiddleTable& tw, uint32_t k) {
   if (N & 1u) {
     const uint32_t half = (N - 1) / 2;
-    return k <= half ? A[k] : conjf2(A[N - k]);
+    return k <= half ? BRP_LD(&A[k]) : conjf2(BRP_LD(&A[N - k]));
   }
-  if (k == Mb) return make_float2(A[0].x - A[0].y, 0.0f);  // Nyquist
-  const float2 zk = A[k], zm = A[(Mb - k) % Mb];
+  if (k == Mb) {  // Nyquist
+    const float2 a0 = BRP_LD(&A[0]);
+    return make_float2(a0.x - a0.y, 0.0f);
+  }
+  const float2 zk = BRP_LD(&A[k]), zm = BRP_LD(&A[(Mb - k) % Mb]);
   return untangle_w(zk, zm, tw_lookup(tw, 2ull * k));  // W_N^k = W_2N^{2k}
 }
 
@@ -106,9 +110,9 @@ __global__ void __launch_bounds__(kThreads) bs_power_kernel(BsPowerArgs a) {
   };
   auto walk = [&](uint32_t t) {
     Walk w{};
-    w.n_s = a.tmpl[t].n_steps;
+    w.n_s = BRP_LD(&a.tmpl[t]).n_steps;
     if (w.n_s > 0) {
-      w.dS = static_cast<float>(a.delta[t]);
+      w.dS = static_cast<float>(BRP_LD(&a.delta[t]));
       w.tk = tw_lookup(a.tw, k0);
       w.sk = tw_lookup(a.tw, kPowStep);
       w.ta = tw_lookup(a.tw, static_cast<uint64_t>(w.n_s) * k0);
@@ -132,8 +136,8 @@ __global__ void __launch_bounds__(kThreads) bs_power_kernel(BsPowerArgs a) {
   };
   auto store = [&](uint32_t t, uint32_t k, float p) {
     const size_t o = static_cast<size_t>(t) * a.ps_stride + k;
-    if (HALF) a.ps16[o] = static_cast<_Float16>(fminf(p, 65504.0f));  // saturate: no inf in the fp16 spectrum
-    else a.ps[o] = p;
+    if (HALF) BRP_ST(&a.ps16[o], static_cast<_Float16>(fminf(p, 65504.0f)));  // saturate: no inf in the fp16 spectrum
+    else BRP_ST(&a.ps[o], p);
   };
   if (!a.pair) {
     Walk w = walk(b);
@@ -158,7 +162,7 @@ __global__ void __launch_bounds__(kThreads) bs_power_kernel(BsPowerArgs a) {
     const bool live = k > 0 && k < real_bins;
     float pa = 0.0f, pb = 0.0f;
     if (live) {
-      const float2 ak = A[k], am = conjf2(A[a.nsamples - k]);
+      const float2 ak = BRP_LD(&A[k]), am = conjf2(BRP_LD(&A[a.nsamples - k]));
       pa = power(make_float2(0.5f * (ak.x + am.x), 0.5f * (ak.y + am.y)), wa);
       if (has_b) pb = power(make_float2(0.5f * (ak.y - am.y), -0.5f * (ak.x - am.x)), wb);
     }
@@ -172,7 +176,7 @@ __global__ void __launch_bounds__(kThreads) bs_power_kernel(BsPowerArgs a) {
 __global__ void __launch_bounds__(kThreads) bs_spec_kernel(const float2* A, uint32_t Mb, uint32_t N, TwiddleTable tw,
                                                            uint32_t fft_size, float2* spec) {
   const uint32_t k = blockIdx.x * kThreads + threadIdx.x;
-  if (k < fft_size) spec[k] = bs_bin(A, Mb, N, tw, k);
+  if (k < fft_size) BRP_ST(&spec[k], bs_bin(A, Mb, N, tw, k));
 }
 
 // inverse transforms: A = DFT(conj(input)); even N: the packed pairs
@@ -181,12 +185,12 @@ __global__ void __launch_bounds__(kThreads) bs_real_out_kernel(const float2* A, 
                                                                float* out, uint32_t n_out) {
   const uint32_t n = blockIdx.x * kThreads + threadIdx.x;
   if (n >= Mb) return;
-  const float2 v = A[n];
+  const float2 v = BRP_LD(&A[n]);
   if (N & 1u) {
-    if (n < n_out) out[n] = v.x * scale;
+    if (n < n_out) BRP_ST(&out[n], v.x * scale);
   } else {
-    if (2 * n < n_out) out[2 * n] = v.x * scale;
-    if (2 * n + 1 < n_out) out[2 * n + 1] = -v.y * scale;
+    if (2 * n < n_out) BRP_ST(&out[2 * n], v.x * scale);
+    if (2 * n + 1 < n_out) BRP_ST(&out[2 * n + 1], -v.y * scale);
   }
 }
 
@@ -198,15 +202,15 @@ __global__ void __launch_bounds__(kThreads) bs_rows_kernel(const float2* H, floa
   if (i >= L1 * L2 * L3) return;
   const uint32_t row = i / L3, k3 = i % L3;
   const uint32_t k1 = row / L2, k2 = row % L2;
-  hp[i] = H[k1 + L1 * k2 + L1 * L2 * k3];
+  BRP_ST(&hp[i], BRP_LD(&H[k1 + L1 * k2 + L1 * L2 * k3]));
 }
 
 }  // namespace
 
 hipError_t launch_bs_rows(const float2* H, float2* hp, uint32_t L1, uint32_t L2, uint32_t L3, hipStream_t s) {
   const uint32_t n = L1 * L2 * L3;
-  hipLaunchKernelGGL(bs_rows_kernel, dim3((n + kThreads - 1) / kThreads), dim3(kThreads), 0, s, H, hp, L1, L2, L3);
-  return hipGetLastError();
+  BRP_LAUNCH(bs_rows_kernel, dim3((n + kThreads - 1) / kThreads), dim3(kThreads), 0, s, H, hp, L1, L2, L3);
+  return launch_status();
 }
 
 uint32_t bs_chirp_in_blocks(uint32_t L) { return (L + kThreads * kPerThread - 1) / (kThreads * kPerThread); }
@@ -216,7 +220,7 @@ hipError_t launch_bs_chirp_in(BsInMode mode, const BsInArgs& a, int batch, uint3
   if (n_partials) *n_partials = grid.x;
   switch (mode) {
 #define BRP_BS_CASE(M) \
-  case M: hipLaunchKernelGGL((bs_chirp_in_kernel<M>), grid, dim3(kThreads), 0, s, a); break;
+  case M: BRP_LAUNCH((bs_chirp_in_kernel<M>), grid, dim3(kThreads), 0, s, a); break;
     BRP_BS_CASE(BS_IN_REAL2)
     BRP_BS_CASE(BS_IN_REAL1)
     BRP_BS_CASE(BS_IN_CONJ)
@@ -225,28 +229,28 @@ hipError_t launch_bs_chirp_in(BsInMode mode, const BsInArgs& a, int batch, uint3
 #undef BRP_BS_CASE
     default: return hipErrorInvalidValue;
   }
-  return hipGetLastError();
+  return launch_status();
 }
 
 hipError_t launch_bs_power(const BsPowerArgs& a, int batch, hipStream_t s) {
   const dim3 grid((a.limit + kThreads * kPowBins - 1) / (kThreads * kPowBins), batch);
-  if (a.ps16) hipLaunchKernelGGL((bs_power_kernel<true>), grid, dim3(kThreads), 0, s, a);
-  else hipLaunchKernelGGL((bs_power_kernel<false>), grid, dim3(kThreads), 0, s, a);
-  return hipGetLastError();
+  if (a.ps16) BRP_LAUNCH((bs_power_kernel<true>), grid, dim3(kThreads), 0, s, a);
+  else BRP_LAUNCH((bs_power_kernel<false>), grid, dim3(kThreads), 0, s, a);
+  return launch_status();
 }
 
 hipError_t launch_bs_spec(const float2* A, uint32_t Mb, uint32_t nsamples, const TwiddleTable& tw, uint32_t fft_size,
                           float2* spec, hipStream_t s) {
-  hipLaunchKernelGGL(bs_spec_kernel, dim3((fft_size + kThreads - 1) / kThreads), dim3(kThreads), 0, s, A, Mb,
+  BRP_LAUNCH(bs_spec_kernel, dim3((fft_size + kThreads - 1) / kThreads), dim3(kThreads), 0, s, A, Mb,
                      nsamples, tw, fft_size, spec);
-  return hipGetLastError();
+  return launch_status();
 }
 
 hipError_t launch_bs_real_out(const float2* A, uint32_t Mb, uint32_t nsamples, float scale, float* out,
                               uint32_t n_out, hipStream_t s) {
-  hipLaunchKernelGGL(bs_real_out_kernel, dim3((Mb + kThreads - 1) / kThreads), dim3(kThreads), 0, s, A, Mb, nsamples,
+  BRP_LAUNCH(bs_real_out_kernel, dim3((Mb + kThreads - 1) / kThreads), dim3(kThreads), 0, s, A, Mb, nsamples,
                      scale, out, n_out);
-  return hipGetLastError();
+  return launch_status();
 }
 
 }  // namespace hipk

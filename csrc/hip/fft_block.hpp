@@ -450,14 +450,14 @@ __device__ __forceinline__ float2 rot_mi(float2 a, uint32_t q) {
 
 template <int L>
 __device__ __forceinline__ void copy_stage_twiddles(float2* tw_lds, const float2* __restrict__ st) {
-  for (int e = threadIdx.x; e < kTwPad<L>; e += blockDim.x) tw_lds[e] = st[e];
+  for (int e = threadIdx.x; e < kTwPad<L>; e += blockDim.x) tw_lds[e] = BRP_LD(&st[e]);
 }
 
 // row-pass stage table: padded W_L^e, then the last stage's q-major block
 // (host: stage_table_rows in hip_engine.cpp)
 template <int L>
 __device__ __forceinline__ void copy_row_twiddles(float2* tw_lds, const float2* __restrict__ st) {
-  for (int e = threadIdx.x; e < kTwPad<L> + kTwRowExtra<L>; e += blockDim.x) tw_lds[e] = st[e];
+  for (int e = threadIdx.x; e < kTwPad<L> + kTwRowExtra<L>; e += blockDim.x) tw_lds[e] = BRP_LD(&st[e]);
 }
 
 }  // namespace hipk

@@ -48,7 +48,7 @@ __global__ void __launch_bounds__(kNcol * tpc_for<L>()) pass1_kernel(Pass1Args a
 
   int c, tj;
   Lay::coords(threadIdx.x, c, tj);
-  if (a.reset != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *a.reset = 0;
+  if (a.reset != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) BRP_ST(a.reset, 0u);
 
   double sum = 0.0, sum_b = 0.0;  // sum_b: the second template of a pair (P1_CHIRP1_PAIR)
   bool pruned = false;
@@ -60,7 +60,7 @@ __global__ void __launch_bounds__(kNcol * tpc_for<L>()) pass1_kernel(Pass1Args a
     }
     __syncthreads();
     const bool fast = a.n_unpadded <= (1u << 23);
-    const TemplateDev td = a.tmpl[b];
+    const TemplateDev td = BRP_LD(&a.tmpl[b]);
     const float* series = a.series + static_cast<size_t>(td.wu) * a.n_unpadded;
     // With padding >= R0 (the first radix) every row n1 >= L/R0 of the
     // tile lies in the zero padding: those rows are neither resampled nor
@@ -94,7 +94,7 @@ __global__ void __launch_bounds__(kNcol * tpc_for<L>()) pass1_kernel(Pass1Args a
       }
       float raw[2 * NU];
 #pragma unroll
-      for (int e = 0; e < 2 * NU; ++e) raw[e] = series[idx[e] < 0 ? 0 : idx[e]];
+      for (int e = 0; e < 2 * NU; ++e) raw[e] = BRP_LD(&series[idx[e] < 0 ? 0 : idx[e]]);
       // per-thread partial sum in float, widened once for the block reduction
       float fsum = 0.0f;
 #pragma unroll
@@ -123,9 +123,9 @@ __global__ void __launch_bounds__(kNcol * tpc_for<L>()) pass1_kernel(Pass1Args a
     const bool fast = a.n_unpadded <= (1u << 23);
     const int ta = kPair ? 2 * b : b;
     const bool has_b = kPair && static_cast<uint32_t>(ta + 1) < a.n_tmpl;
-    const TemplateDev td = a.tmpl[ta];
+    const TemplateDev td = BRP_LD(&a.tmpl[ta]);
     TemplateDev tdb = td;
-    if (has_b) tdb = a.tmpl[ta + 1];
+    if (has_b) tdb = BRP_LD(&a.tmpl[ta + 1]);
     const float* series = a.series + static_cast<size_t>(td.wu) * a.n_unpadded;
     const float* series_b = a.series + static_cast<size_t>(tdb.wu) * a.n_unpadded;
     const int last = static_cast<int>(a.n_unpadded) - 1;
@@ -138,7 +138,7 @@ __global__ void __launch_bounds__(kNcol * tpc_for<L>()) pass1_kernel(Pass1Args a
       if (m >= t.n_steps) return 0.0f;
       const float dt = resamp_del_t(m, t.p, lut_s, lut_c);
       const int i = min(max(fast ? resamp_nearest_f(m, dt) : resamp_nearest(m, dt), 0), last);
-      return ser[i] - t.mu0;
+      return BRP_LD(&ser[i]) - t.mu0;
     };
     auto sample = [&](uint32_t m) { return sample_of(td, series, m); };
     float fsum = 0.0f, fsum_b = 0.0f;
@@ -164,19 +164,19 @@ __global__ void __launch_bounds__(kNcol * tpc_for<L>()) pass1_kernel(Pass1Args a
   } else if (MODE == P1_REAL) {
     for (int r = tj; r < L; r += TPC) {
       const uint32_t n = r * a.L2L3 + col_base + c;
-      const float x0 = (2 * n < a.n_real) ? a.real_in[2 * n] : 0.0f;
-      const float x1 = (2 * n + 1 < a.n_real) ? a.real_in[2 * n + 1] : 0.0f;
+      const float x0 = (2 * n < a.n_real) ? BRP_LD(&a.real_in[2 * n]) : 0.0f;
+      const float x1 = (2 * n + 1 < a.n_real) ? BRP_LD(&a.real_in[2 * n + 1]) : 0.0f;
       data[Lay::idx(r, c)] = make_float2(x0, x1);
     }
   } else {
     for (int r = tj; r < L; r += TPC) {
       const uint32_t n = r * a.L2L3 + col_base + c;
-      const float2 v = a.cplx_in[static_cast<size_t>(b) * M + n];
+      const float2 v = BRP_LD(&a.cplx_in[static_cast<size_t>(b) * M + n]);
       data[Lay::idx(r, c)] = MODE == P1_COMPLEX_CONJ ? conjf2(v) : v;
     }
   }
   copy_stage_twiddles<L>(twl, a.tb.st1);
-  for (int k1 = threadIdx.x; k1 < L; k1 += NT) two[k1] = a.tb.p1[n2 * L + k1];  // W_{L1 L2}^{n2 k1}
+  for (int k1 = threadIdx.x; k1 < L; k1 += NT) two[k1] = BRP_LD(&a.tb.p1[n2 * L + k1]);  // W_{L1 L2}^{n2 k1}
   __syncthreads();
   if (pruned) BlockFFT<L, kNcol, TPC, false>::run_pruned(data, twl);
   else BlockFFT<L, kNcol, TPC, false>::run(data, twl);
@@ -184,18 +184,18 @@ __global__ void __launch_bounds__(kNcol * tpc_for<L>()) pass1_kernel(Pass1Args a
   float2* out = a.out + static_cast<size_t>(b) * M;
   for (int k1 = tj; k1 < L; k1 += TPC) {
     const float2 v = cmul(data[Lay::idx(k1, c)], two[k1]);
-    out[static_cast<size_t>(k1) * a.L2L3 + col_base + c] = v;
+    BRP_ST(&out[static_cast<size_t>(k1) * a.L2L3 + col_base + c], v);
   }
   if (MODE == P1_RESAMPLE || MODE == P1_CHIRP2 || MODE == P1_CHIRP1) {
     const double tot = block_sum<NT>(sum, red);
-    if (threadIdx.x == 0) a.partials[static_cast<size_t>(b) * gridDim.x + blockIdx.x] = tot;
+    if (threadIdx.x == 0) BRP_ST(&a.partials[static_cast<size_t>(b) * gridDim.x + blockIdx.x], tot);
   } else if (MODE == P1_CHIRP1_PAIR) {  // partial sums per template (2b, 2b + 1)
     const double tot = block_sum<NT>(sum, red);
     const double tot_b = block_sum<NT>(sum_b, red);
     if (threadIdx.x == 0) {
-      a.partials[static_cast<size_t>(2 * b) * gridDim.x + blockIdx.x] = tot;
+      BRP_ST(&a.partials[static_cast<size_t>(2 * b) * gridDim.x + blockIdx.x], tot);
       if (static_cast<uint32_t>(2 * b + 1) < a.n_tmpl)
-        a.partials[static_cast<size_t>(2 * b + 1) * gridDim.x + blockIdx.x] = tot_b;
+        BRP_ST(&a.partials[static_cast<size_t>(2 * b + 1) * gridDim.x + blockIdx.x], tot_b);
     }
   }
 }
@@ -253,13 +253,13 @@ pass1_pruned3_kernel(Pass1Args a) {
   const size_t M = static_cast<size_t>(L) * a.L2L3;
   const int c = threadIdx.x % kNcol;
   const int tj = threadIdx.x / kNcol;
-  if (a.reset != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *a.reset = 0;
+  if (a.reset != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) BRP_ST(a.reset, 0u);
 
   // the template, the sine LUT and the twiddle tables are loaded together
   // before the first LDS write (one memory round trip instead of three ahead
   // of the gather)
   static_assert(kLutSize <= NT && L <= NT, "one LUT / table entry per thread");
-  const TemplateDev td = a.tmpl[b];
+  const TemplateDev td = BRP_LD(&a.tmpl[b]);
   const int tid = static_cast<int>(threadIdx.x);
   float ls = 0.0f, lc = 0.0f;
   float2 wv = make_float2(0.0f, 0.0f), tv = wv;
@@ -268,8 +268,8 @@ pass1_pruned3_kernel(Pass1Args a) {
     lc = kCosLut[tid];
   }
   if (tid < L) {
-    wv = a.tb.st1[tid + (tid >> 4)];
-    tv = a.tb.p1[n2 * L + tid];
+    wv = BRP_LD(&a.tb.st1[tid + (tid >> 4)]);
+    tv = BRP_LD(&a.tb.p1[n2 * L + tid]);
   }
   if (tid < kLutSize) {
     lut_s[tid] = ls;
@@ -307,7 +307,8 @@ pass1_pruned3_kernel(Pass1Args a) {
   }
   float raw[2 * R2];
 #pragma unroll
-  for (int e = 0; e < 2 * R2; ++e) raw[e] = series[idx[e] < 0 ? 0 : idx[e]];
+  for (int e = 0; e < 2 * R2; ++e)
+    raw[e] = BRP_LD(&series[BRP_INJECT_AT(idx[e] < 0 ? 0 : idx[e], last + 17, kInjPass1)]);
   float fsum = 0.0f;
   float2 x[R2];
 #pragma unroll
@@ -342,11 +343,11 @@ pass1_pruned3_kernel(Pass1Args a) {
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int k1 = tj + NB3 * q;
-      out[static_cast<size_t>(k1) * a.L2L3] = cmul(z[q], lds_ld64(&two[k1]));
+      BRP_ST(&out[static_cast<size_t>(k1) * a.L2L3], cmul(z[q], lds_ld64(&two[k1])));
     }
   }
   const double tot = block_sum<NT>(static_cast<double>(fsum), red);
-  if (threadIdx.x == 0) a.partials[static_cast<size_t>(b) * gridDim.x + blockIdx.x] = tot;
+  if (threadIdx.x == 0) BRP_ST(&a.partials[static_cast<size_t>(b) * gridDim.x + blockIdx.x], tot);
 }
 
 // ------------------------------------------------------------------ pass 2
@@ -361,11 +362,11 @@ __device__ __forceinline__ void reduce_delta(const Pass2Args& a, uint32_t b, dou
     if (tpt > 1 && t >= a.n_tmpl) break;  // uniform
     const double* pp = a.partials + static_cast<size_t>(t) * a.n_partials;
     double part = 0.0;
-    for (uint32_t i = threadIdx.x; i < a.n_partials; i += NT) part += pp[i];
+    for (uint32_t i = threadIdx.x; i < a.n_partials; i += NT) part += BRP_LD(&pp[i]);
     const double tot = block_sum<NT>(part, red);
     if (threadIdx.x == 0) {
-      const uint32_t n_s = a.tmpl[t].n_steps;
-      a.delta[t] = n_s ? tot / static_cast<double>(n_s) : 0.0;
+      const uint32_t n_s = BRP_LD(&a.tmpl[t]).n_steps;
+      BRP_ST(&a.delta[t], n_s ? tot / static_cast<double>(n_s) : 0.0);
     }
   }
 }
@@ -411,13 +412,13 @@ __global__ void __launch_bounds__(kNcol * tpc_for<L>(), kMinWaves) pass2_kernel(
   if (tile < ntiles) {
     const float2* src = a.buf + tile_base(tile);
 #pragma unroll
-    for (int u = 0; u < kPer; ++u) pre[u] = src[static_cast<size_t>(tj + u * TPC) * a.L3 + c];
+    for (int u = 0; u < kPer; ++u) pre[u] = BRP_LD(&src[static_cast<size_t>(tj + u * TPC) * a.L3 + c]);
   }
   {
     copy_stage_twiddles<L>(twl, a.tb.st2);
     const uint32_t nhi = (a.L2L3 + kLo - 1) / kLo;
-    for (int i = threadIdx.x; i < kLo; i += NT) lo[i] = a.tb.p2lo[i];
-    for (uint32_t i = threadIdx.x; i < nhi; i += NT) hi[i] = a.tb.p2hi[i];
+    for (int i = threadIdx.x; i < kLo; i += NT) lo[i] = BRP_LD(&a.tb.p2lo[i]);
+    for (uint32_t i = threadIdx.x; i < nhi; i += NT) hi[i] = BRP_LD(&a.tb.p2hi[i]);
   }
   while (tile < ntiles) {
     const uint32_t b = tile / per_b, rem = tile % per_b;
@@ -427,12 +428,12 @@ __global__ void __launch_bounds__(kNcol * tpc_for<L>(), kMinWaves) pass2_kernel(
 #pragma unroll
     for (int u = 0; u < kPer; ++u) data[Lay::idx(tj + u * TPC, c)] = pre[u];
     // W_M^{n3 (k1 + L1 k2)} = W_M^{n3 k1} * W_{L2 L3}^{n3 k2}
-    const float2 wc = a.tb.p2col[k1 * a.L3 + n3];
+    const float2 wc = BRP_LD(&a.tb.p2col[k1 * a.L3 + n3]);
     const uint32_t next = tile + gridDim.x;
     if (next < ntiles) {  // in flight during this tile's FFT and stores
       const float2* src = a.buf + tile_base(next);
 #pragma unroll
-      for (int u = 0; u < kPer; ++u) pre[u] = src[static_cast<size_t>(tj + u * TPC) * a.L3 + c];
+      for (int u = 0; u < kPer; ++u) pre[u] = BRP_LD(&src[static_cast<size_t>(tj + u * TPC) * a.L3 + c]);
     }
     __syncthreads();
     BlockFFT<L, kNcol, TPC, false>::run(data, twl);
@@ -442,7 +443,7 @@ __global__ void __launch_bounds__(kNcol * tpc_for<L>(), kMinWaves) pass2_kernel(
       const uint32_t e = n3 * static_cast<uint32_t>(k2);  // < L2*L3
       float2 v = data[Lay::idx(k2, c)];
       v = cmul(v, cmul(wc, cmul(hi[e >> kP2LoBits], lo[e & (kLo - 1)])));
-      base[static_cast<size_t>(k2) * a.L3 + c] = v;
+      BRP_ST(&base[static_cast<size_t>(k2) * a.L3 + c], v);
     }
     if (a.partials != nullptr && rem == 0) reduce_delta<NT>(a, b, red);
     __syncthreads();  // LDS tile free for the next iteration
@@ -500,10 +501,10 @@ __global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_
   if (tile < ntiles) {
     const float2* src = tile_base(tile);
 #pragma unroll
-    for (int u = 0; u < 16; ++u) pre[u] = *at(src, u);
+    for (int u = 0; u < 16; ++u) pre[u] = BRP_LD(at(src, u));
   }
   {
-    for (int e = threadIdx.x; e < L; e += NT) wl[e] = a.tb.st2[e + (e >> 4)];
+    for (int e = threadIdx.x; e < L; e += NT) wl[e] = BRP_LD(&a.tb.st2[e + (e >> 4)]);
   }
   __syncthreads();
   while (tile < ntiles) {
@@ -512,7 +513,7 @@ __global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_
     const uint32_t k1 = __builtin_amdgcn_readfirstlane(rem / nblk3);
     const uint32_t n3 = (rem % nblk3) * kNcol + c;
     float2* base = const_cast<float2*>(tile_base(tile));
-    const float2 wc = a.tb.p2col[k1 * a.L3 + n3];
+    const float2 wc = BRP_LD(&a.tb.p2col[k1 * a.L3 + n3]);
     // stage 1 (radix R1, no twiddles) on the loaded rows: butterfly
     // j = tj + R1 v holds rows j + 16 q = tj + TPC (v + NB1 q)
 #pragma unroll
@@ -529,7 +530,7 @@ __global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_
     if (next < ntiles) {  // in flight during the exchange, stage 2 and the stores
       const float2* src = tile_base(next);
 #pragma unroll
-      for (int u = 0; u < 16; ++u) pre[u] = *at(src, u);
+      for (int u = 0; u < 16; ++u) pre[u] = BRP_LD(at(src, u));
     }
     __syncthreads();
     // stage 2 (radix 16, Ns = R1): butterfly tj reads rows tj + R1 q, twiddle W_L^{tj q}
@@ -545,13 +546,13 @@ __global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_
       // W_{L1 L2}^{k1 m2} (p1 table, [m2][k1]), exact at q = 0 and 8 and
       // stepped by W_{L1 L2}^{k1 TPC} in between (as the forward twiddles)
       const float2* p1c = a.tb.p1 + k1;
-      const float2 step = p1c[static_cast<uint32_t>(TPC) * a.L1];
-      float2 t0 = p1c[static_cast<uint32_t>(tj) * a.L1];
-      float2 t8 = p1c[static_cast<uint32_t>(tj + 8 * TPC) * a.L1];
+      const float2 step = BRP_LD(&p1c[static_cast<uint32_t>(TPC) * a.L1]);
+      float2 t0 = BRP_LD(&p1c[static_cast<uint32_t>(tj) * a.L1]);
+      float2 t8 = BRP_LD(&p1c[static_cast<uint32_t>(tj + 8 * TPC) * a.L1]);
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
-        *const_cast<float2*>(at(base, q)) = cmul(y[q], t0);
-        *const_cast<float2*>(at(base, q + 8)) = cmul(y[q + 8], t8);
+        BRP_ST(const_cast<float2*>(at(base, q)), cmul(y[q], t0));
+        BRP_ST(const_cast<float2*>(at(base, q + 8)), cmul(y[q + 8], t8));
         t0 = cmul(t0, step);
         t8 = cmul(t8, step);
       }
@@ -559,14 +560,14 @@ __global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_
       continue;
     }
     // outputs k2 = tj + TPC q
-    auto wexact = [&](uint32_t e) { return cmul(hi[e >> kP2LoBits], lo[e & (kLo - 1)]); };
+    auto wexact = [&](uint32_t e) { return cmul(BRP_LD(&hi[e >> kP2LoBits]), BRP_LD(&lo[e & (kLo - 1)])); };
     const float2 step = wexact(n3 * static_cast<uint32_t>(TPC));
     float2 t0 = cmul(wc, wexact(n3 * static_cast<uint32_t>(tj)));
     float2 t8 = cmul(wc, wexact(n3 * static_cast<uint32_t>(tj + 8 * TPC)));
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
-      *const_cast<float2*>(at(base, q)) = cmul(y[q], t0);
-      *const_cast<float2*>(at(base, q + 8)) = cmul(y[q + 8], t8);
+      BRP_ST(const_cast<float2*>(at(base, q)), cmul(y[q], t0));
+      BRP_ST(const_cast<float2*>(at(base, q + 8)), cmul(y[q + 8], t8));
       t0 = cmul(t0, step);
       t8 = cmul(t8, step);
     }
@@ -650,6 +651,12 @@ struct ChirpWalk {
     return w;
   }
 };
+// stand-in for the modes without a reverse chirp: the table is unset there
+// (period 0, no entries), so no lookup may be emitted at all
+struct NoChirpWalk {
+  __device__ __forceinline__ NoChirpWalk(const TwiddleTable&, uint64_t, uint64_t) {}
+  __device__ __forceinline__ float2 next(int) { return make_float2(1.0f, 0.0f); }
+};
 
 // Register-staged pass 2 for L = 16 * R1 with R1 not a divisor of 16 (96, 144,
 // 160, 192, 240, 288, 320: the chirp-z plans' lengths), two Stockham stages in
@@ -706,9 +713,9 @@ __global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_
   if (tile < ntiles) {
     const float2* src = tile_base(tile);
 #pragma unroll
-    for (int q = 0; q < 16; ++q) pre[q] = *ld_at(src, q);
+    for (int q = 0; q < 16; ++q) pre[q] = BRP_LD(ld_at(src, q));
   }
-  for (int e = threadIdx.x; e < L; e += NT) wl[e] = a.tb.st2[e + (e >> 4)];
+  for (int e = threadIdx.x; e < L; e += NT) wl[e] = BRP_LD(&a.tb.st2[e + (e >> 4)]);
   __syncthreads();
   while (tile < ntiles) {
     const uint32_t b = __builtin_amdgcn_readfirstlane(tile / per_b);
@@ -716,7 +723,7 @@ __global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_
     const uint32_t k1 = __builtin_amdgcn_readfirstlane(rem / nblk3);
     const uint32_t n3 = (rem % nblk3) * kNcol + c;
     float2* base = const_cast<float2*>(tile_base(tile));
-    const float2 wc = a.tb.p2col[k1 * a.L3 + n3];
+    const float2 wc = BRP_LD(&a.tb.p2col[k1 * a.L3 + n3]);
     // stage 1 (radix 16, Ns = 1): butterfly tj, outputs rows 16 tj + q
     Dft<16>::run(pre);
 #pragma unroll
@@ -725,7 +732,7 @@ __global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_
     if (next < ntiles) {  // in flight during the exchange, stage 2 and the stores
       const float2* src = tile_base(next);
 #pragma unroll
-      for (int q = 0; q < 16; ++q) pre[q] = *ld_at(src, q);
+      for (int q = 0; q < 16; ++q) pre[q] = BRP_LD(ld_at(src, q));
     }
     __syncthreads();
     // stage 2 (radix R1, Ns = 16): butterfly j reads rows j + 16 q, twiddle W_L^{j q}
@@ -747,7 +754,7 @@ __global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_
       // W_{L1 L2}^{k1 m2} (p1 table, [m2][k1]), exact every 8 rows and
       // stepped by W_{L1 L2}^{16 k1} in between (as the forward twiddles)
       const float2* p1c = a.tb.p1 + k1;
-      const float2 step = p1c[16u * a.L1];
+      const float2 step = BRP_LD(&p1c[16u * a.L1]);
 #pragma unroll
       for (int v = 0; v < NB2; ++v) {
         const int j = tj + TPC * v;
@@ -756,8 +763,8 @@ __global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_
           float2 t = make_float2(1.f, 0.f);
 #pragma unroll
           for (int q = 0; q < R1; ++q) {
-            if (q % 8 == 0) t = p1c[static_cast<uint32_t>(j + 16 * q) * a.L1];
-            *reinterpret_cast<float2*>(reinterpret_cast<char*>(base + q * st_step) + st_off) = cmul(y[v][q], t);
+            if (q % 8 == 0) t = BRP_LD(&p1c[static_cast<uint32_t>(j + 16 * q) * a.L1]);
+            BRP_ST(reinterpret_cast<float2*>(reinterpret_cast<char*>(base + q * st_step) + st_off), cmul(y[v][q], t));
             t = cmul(t, step);
           }
         }
@@ -767,7 +774,7 @@ __global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_
     }
     // outputs k2 = j + 16 q with W_M^{n3 (k1 + L1 k2)} = wc * W_{L2L3}^{n3 k2},
     // exact every 8 rows and stepped by W_{L2L3}^{16 n3} in between
-    auto wexact = [&](uint32_t e) { return cmul(hi[e >> kP2LoBits], lo[e & (kLo - 1)]); };
+    auto wexact = [&](uint32_t e) { return cmul(BRP_LD(&hi[e >> kP2LoBits]), BRP_LD(&lo[e & (kLo - 1)])); };
     const float2 step = wexact(n3 * 16u);
 #pragma unroll
     for (int v = 0; v < NB2; ++v) {
@@ -778,7 +785,7 @@ __global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_
 #pragma unroll
         for (int q = 0; q < R1; ++q) {
           if (q % 8 == 0) t = cmul(wc, wexact(n3 * static_cast<uint32_t>(j + 16 * q)));
-          *reinterpret_cast<float2*>(reinterpret_cast<char*>(base + q * st_step) + st_off) = cmul(y[v][q], t);
+          BRP_ST(reinterpret_cast<float2*>(reinterpret_cast<char*>(base + q * st_step) + st_off), cmul(y[v][q], t));
           t = cmul(t, step);
         }
       }
@@ -823,7 +830,7 @@ __global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_
   const int tj = threadIdx.x / kNcol;
   auto col = [](int r, int cc) { return r * kNcol + cc; };
   auto tw1 = [&](int e) { return wl[(16 * e) % L]; };  // W_{R1}^e = W_L^{16 e}
-  if (a.reset != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *a.reset = 0;
+  if (a.reset != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) BRP_ST(a.reset, 0u);
 
   float2 x[16];
   double sum = 0.0, sum_b = 0.0;  // sum_b: the second template of a pair (P1_CHIRP1_PAIR)
@@ -837,7 +844,7 @@ __global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_
     }
     __syncthreads();
     const bool fast = a.n_unpadded <= (1u << 23);
-    const TemplateDev td = a.tmpl[b];
+    const TemplateDev td = BRP_LD(&a.tmpl[b]);
     const float* series = a.series + static_cast<size_t>(td.wu) * a.n_unpadded;
     const int last = static_cast<int>(a.n_unpadded) - 1;
     int idx[32];
@@ -857,7 +864,7 @@ __global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_
     }
     float raw[32];
 #pragma unroll
-    for (int e = 0; e < 32; ++e) raw[e] = series[idx[e] < 0 ? 0 : idx[e]];
+    for (int e = 0; e < 32; ++e) raw[e] = BRP_LD(&series[idx[e] < 0 ? 0 : idx[e]]);
     float fsum = 0.0f;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
@@ -873,7 +880,7 @@ __global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_
     const size_t ld_step = static_cast<size_t>(R1) * a.L2L3;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
-      const float2 v = src[q * ld_step];
+      const float2 v = BRP_LD(&src[q * ld_step]);
       x[q] = MODE == P1_COMPLEX_CONJ ? conjf2(v) : v;
     }
   } else {
@@ -888,9 +895,9 @@ __global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_
     const bool fast = a.n_unpadded <= (1u << 23);
     const int ta = kPair ? 2 * b : b;
     const bool has_b = kPair && static_cast<uint32_t>(ta + 1) < a.n_tmpl;
-    const TemplateDev td = a.tmpl[ta];
+    const TemplateDev td = BRP_LD(&a.tmpl[ta]);
     TemplateDev tdb = td;
-    if (has_b) tdb = a.tmpl[ta + 1];
+    if (has_b) tdb = BRP_LD(&a.tmpl[ta + 1]);
     const float* series = a.series + static_cast<size_t>(td.wu) * a.n_unpadded;
     const float* series_b = a.series + static_cast<size_t>(tdb.wu) * a.n_unpadded;
     const int last = static_cast<int>(a.n_unpadded) - 1;
@@ -898,7 +905,7 @@ __global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_
       if (m >= t.n_steps) return 0.0f;
       const float dt = resamp_del_t(m, t.p, lut_s, lut_c);
       const int i = min(max(fast ? resamp_nearest_f(m, dt) : resamp_nearest(m, dt), 0), last);
-      return ser[i] - t.mu0;
+      return BRP_LD(&ser[i]) - t.mu0;
     };
     (void)sample_of;
     // three phases as the resampling gather: the nearest indices of all 16
@@ -908,7 +915,7 @@ __global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_
     const uint32_t D = static_cast<uint32_t>(R1) * a.L2L3;
     // rows q >= qw of the whole wave lie in the zero padding (n >= Mb, about
     // half the rows): their gathers and chirp factors are skipped uniformly
-    const uint32_t qw = wave_max_u32(n0 < a.Mb ? min(16u, (a.Mb - n0 + D - 1) / D) : 0u);
+    const uint32_t qw = wave_max_u32<5>(n0 < a.Mb ? min(16u, (a.Mb - n0 + D - 1) / D) : 0u);
     int idx[32];
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
@@ -931,7 +938,7 @@ __global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
       const float* ser = (MODE == P1_CHIRP2 || e % 2 == 0) ? series : series_b;
-      raw[e] = ser[idx[e] < 0 ? 0 : idx[e]];
+      raw[e] = BRP_LD(&ser[idx[e] < 0 ? 0 : idx[e]]);
     }
 #pragma unroll
     for (int e = 16; e < 32; ++e) raw[e] = 0.0f;
@@ -939,7 +946,7 @@ __global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_
 #pragma unroll
       for (int e = 16; e < 32; ++e) {
         const float* ser = (MODE == P1_CHIRP2 || e % 2 == 0) ? series : series_b;
-        raw[e] = ser[idx[e] < 0 ? 0 : idx[e]];
+        raw[e] = BRP_LD(&ser[idx[e] < 0 ? 0 : idx[e]]);
       }
     }
     float fsum = 0.0f, fsum_b = 0.0f;
@@ -965,7 +972,7 @@ __global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_
     sum = static_cast<double>(fsum);
     sum_b = static_cast<double>(fsum_b);
   }
-  for (int e = threadIdx.x; e < L; e += NT) wl[e] = a.tb.st1[e + (e >> 4)];
+  for (int e = threadIdx.x; e < L; e += NT) wl[e] = BRP_LD(&a.tb.st1[e + (e >> 4)]);
   // stage 1 (radix 16, Ns = 1): butterfly tj, outputs rows 16 tj + q
   Dft<16>::run(x);
 #pragma unroll
@@ -980,7 +987,8 @@ __global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_
     const int j = tj + TPC * v;
     if (j < 16) {
       // P1_REV_CHIRP: chirp factors of the outputs n = (j + 16 q) L2L3 + col
-      ChirpWalk cw(a.chirp, static_cast<uint64_t>(j) * a.L2L3 + col_base + c, 16ull * a.L2L3);
+      std::conditional_t<MODE == P1_REV_CHIRP, ChirpWalk, NoChirpWalk> cw(
+          a.chirp, static_cast<uint64_t>(j) * a.L2L3 + col_base + c, 16ull * a.L2L3);
       float2 y[R1];
 #pragma unroll
       for (int q = 0; q < R1; ++q) y[q] = data[col(j + 16 * q, c)];
@@ -994,23 +1002,23 @@ __global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_
           // natural-order n: conj(.) * w_n / L for n < Mb (the length-Mb DFT)
           const uint32_t n = static_cast<uint32_t>(k1) * a.L2L3 + col_base + c;
           const float2 w = cw.next(q);
-          if (n < a.Mb) out[static_cast<size_t>(k1) * a.L2L3] = cscale(cmul(conjf2(y[q]), w), a.scale);
+          if (n < a.Mb) BRP_ST(&out[static_cast<size_t>(k1) * a.L2L3], cscale(cmul(conjf2(y[q]), w), a.scale));
         } else {
-          out[static_cast<size_t>(k1) * a.L2L3] = cmul(y[q], two[k1]);
+          BRP_ST(&out[static_cast<size_t>(k1) * a.L2L3], cmul(y[q], BRP_LD(&two[k1])));
         }
       }
     }
   }
   if constexpr (MODE == P1_CHIRP2 || MODE == P1_CHIRP1 || MODE == P1_RESAMPLE) {
     const double tot = block_sum<NT>(sum, red);
-    if (threadIdx.x == 0) a.partials[static_cast<size_t>(b) * gridDim.x + blockIdx.x] = tot;
+    if (threadIdx.x == 0) BRP_ST(&a.partials[static_cast<size_t>(b) * gridDim.x + blockIdx.x], tot);
   } else if constexpr (MODE == P1_CHIRP1_PAIR) {  // partial sums per template (2b, 2b + 1)
     const double tot = block_sum<NT>(sum, red);
     const double tot_b = block_sum<NT>(sum_b, red);
     if (threadIdx.x == 0) {
-      a.partials[static_cast<size_t>(2 * b) * gridDim.x + blockIdx.x] = tot;
+      BRP_ST(&a.partials[static_cast<size_t>(2 * b) * gridDim.x + blockIdx.x], tot);
       if (static_cast<uint32_t>(2 * b + 1) < a.n_tmpl)
-        a.partials[static_cast<size_t>(2 * b + 1) * gridDim.x + blockIdx.x] = tot_b;
+        BRP_ST(&a.partials[static_cast<size_t>(2 * b + 1) * gridDim.x + blockIdx.x], tot_b);
     }
   }
 }
@@ -1062,15 +1070,16 @@ struct P3Emit {
   }
   // stores bin k's power; returns the value the spectrum holds (fp16-rounded in P3_POWER16)
   __device__ __forceinline__ float store(uint32_t k, float p) const {
-    const size_t o = static_cast<size_t>(b) * a.ps_stride + k;
+    const size_t o = BRP_INJECT_AT(static_cast<size_t>(b) * a.ps_stride + k,
+                                   static_cast<size_t>(gridDim.y) * a.ps_stride + 16, kInjPass3);
     // fp16 spectrum (config 5) saturates at the largest finite half: a strong
     // line stays a (clamped) candidate instead of an inf in the sums
     if (MODE == P3_POWER16) {
       const _Float16 h = static_cast<_Float16>(fminf(p, 65504.0f));
-      a.ps16[o] = h;
+      BRP_ST(&a.ps16[o], h);
       return static_cast<float>(h);
     }
-    a.ps[o] = p;
+    BRP_ST(&a.ps[o], p);
     return p;
   }
   // the spectrum value written for bin k (0 for bins past the limit: the
@@ -1078,7 +1087,7 @@ struct P3Emit {
   __device__ __forceinline__ float operator()(uint32_t k, float2 x, float2 tk, float2 ta) const {
     if (k >= a.limit) return 0.0f;
     if (kPower) return store(k, power(k, x, tk, ta));
-    a.spec[k] = x;
+    BRP_ST(&a.spec[k], x);
     return 0.0f;
   }
   // Nyquist bin M: X_M = Re Z_0 - Im Z_0
@@ -1093,7 +1102,7 @@ struct P3Emit {
       const float pm = (x.x * x.x + x.y * x.y) * a.norm;
       return store(a.M, pm);
     }
-    a.spec[a.M] = x;
+    BRP_ST(&a.spec[a.M], x);
     return 0.0f;
   }
 };
@@ -1148,9 +1157,9 @@ __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Arg
 #pragma unroll
     for (int i = 0; i < kTwIt; ++i) {
       const int e = static_cast<int>(threadIdx.x) + i * NT;
-      twv[i] = e < kTwN ? a.tb.st3[e] : make_float2(0.0f, 0.0f);
+      twv[i] = e < kTwN ? BRP_LD(&a.tb.st3[e]) : make_float2(0.0f, 0.0f);
     }
-    if (threadIdx.x < kT4) t4v = a.tb.p3[threadIdx.x];
+    if (threadIdx.x < kT4) t4v = BRP_LD(&a.tb.p3[threadIdx.x]);
   };
   if constexpr (!kRegStage1) {
     int slot, tj;
@@ -1162,7 +1171,7 @@ __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Arg
     static_assert((L / 2) % TPC == 0, "whole row-load iterations");
     float4 rv[kRowIt];
 #pragma unroll
-    for (int u = 0; u < kRowIt; ++u) rv[u] = src[tj + u * TPC];
+    for (int u = 0; u < kRowIt; ++u) rv[u] = BRP_LD(&src[tj + u * TPC]);
     load_tables();
 #pragma unroll
     for (int u = 0; u < kRowIt; ++u) {
@@ -1180,7 +1189,7 @@ __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Arg
 #pragma unroll
     for (int u = 0; u < kBf0 / TPC; ++u)
 #pragma unroll
-      for (int q = 0; q < R0; ++q) v[u][q] = src[tj + u * TPC + q * kBf0];
+      for (int q = 0; q < R0; ++q) v[u][q] = BRP_LD(&src[tj + u * TPC + q * kBf0]);
     load_tables();
 #pragma unroll
     for (int u = 0; u < kBf0 / TPC; ++u) {
@@ -1200,8 +1209,8 @@ __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Arg
   double delta = 0.0;
   uint32_t n_s = 0;
   if (MODE == P3_POWER || MODE == P3_POWER16) {
-    n_s = a.tmpl[b].n_steps;
-    delta = a.delta[b];
+    n_s = BRP_LD(&a.tmpl[b]).n_steps;
+    delta = BRP_LD(&a.delta[b]);
   }
   // per-row twiddle constants of the untangle phase, fetched before the FFT so
   // their latency hides under it
@@ -1273,7 +1282,7 @@ __global__ void __launch_bounds__(ROWS * tpc_for<L>()) pass3_plain_kernel(Pass3P
     int slot, tj;
     Lay::coords(threadIdx.x, slot, tj);
     const float2* src = a.buf + row_base(c0 + slot, a.L1, a.L2, a.L3);
-    for (int r = tj; r < L; r += TPC) data[Lay::idx(r, slot)] = src[r];
+    for (int r = tj; r < L; r += TPC) data[Lay::idx(r, slot)] = BRP_LD(&src[r]);
   }
   copy_row_twiddles<L>(twl, a.tb.st3);
   __syncthreads();
@@ -1286,8 +1295,8 @@ __global__ void __launch_bounds__(ROWS * tpc_for<L>()) pass3_plain_kernel(Pass3P
   for (int k3 = t; k3 < L; k3 += kStreams) {
     const float2 z = data[Lay::idx(k3, s)];
     const size_t n = c + static_cast<size_t>(a.C) * k3;
-    if (2 * n < a.n_out) a.real_out[2 * n] = z.x * a.scale;
-    if (2 * n + 1 < a.n_out) a.real_out[2 * n + 1] = -z.y * a.scale;
+    if (2 * n < a.n_out) BRP_ST(&a.real_out[2 * n], z.x * a.scale);
+    if (2 * n + 1 < a.n_out) BRP_ST(&a.real_out[2 * n + 1], -z.y * a.scale);
   }
 }
 
@@ -1310,7 +1319,7 @@ __global__ void __launch_bounds__(ROWS * tpc_for<L>()) pass3_cplx_kernel(Pass3Cp
     int slot, tj;
     Lay::coords(threadIdx.x, slot, tj);
     const float2* src = buf + row_base(c0 + slot, a.L1, a.L2, a.L3);
-    for (int r = tj; r < L; r += TPC) data[Lay::idx(r, slot)] = src[r];
+    for (int r = tj; r < L; r += TPC) data[Lay::idx(r, slot)] = BRP_LD(&src[r]);
   }
   copy_row_twiddles<L>(twl, a.tb.st3);
   __syncthreads();
@@ -1324,12 +1333,12 @@ __global__ void __launch_bounds__(ROWS * tpc_for<L>()) pass3_cplx_kernel(Pass3Cp
     const float2 z = data[Lay::idx(k3, s)];
     const uint32_t n = c + a.C * static_cast<uint32_t>(k3);
     if (MODE == C3_PLAIN) {
-      out[n] = z;
+      BRP_ST(&out[n], z);
     } else if (MODE == C3_MULCONJ) {
-      out[n] = conjf2(cmul(z, a.h[n]));
+      BRP_ST(&out[n], conjf2(cmul(z, BRP_LD(&a.h[n]))));
     } else if (n < a.n_out) {
       const float2 w = tw_lookup(a.chirp, static_cast<uint64_t>(n) * n);
-      out[n] = cscale(cmul(conjf2(z), w), a.scale);
+      BRP_ST(&out[n], cscale(cmul(conjf2(z), w), a.scale));
     }
   }
 }
@@ -1361,7 +1370,7 @@ __global__ void __launch_bounds__(ROWS * tpc_for<L>()) pass3_mid_kernel(Pass3Mid
   {
     float2 v[kPer];
 #pragma unroll
-    for (int u = 0; u < kPer; ++u) v[u] = buf[rbase + tj + u * TPC];
+    for (int u = 0; u < kPer; ++u) v[u] = BRP_LD(&buf[rbase + tj + u * TPC]);
     copy_row_twiddles<L>(twl, a.tb.st3);
 #pragma unroll
     for (int u = 0; u < kPer; ++u) data[Lay::idx(tj + u * TPC, slot)] = v[u];
@@ -1371,7 +1380,7 @@ __global__ void __launch_bounds__(ROWS * tpc_for<L>()) pass3_mid_kernel(Pass3Mid
   {
     float2 h[kPer];
 #pragma unroll
-    for (int u = 0; u < kPer; ++u) h[u] = a.hp[rbase + tj + u * TPC];
+    for (int u = 0; u < kPer; ++u) h[u] = BRP_LD(&a.hp[rbase + tj + u * TPC]);
 #pragma unroll
     for (int u = 0; u < kPer; ++u) {
       const int e = Lay::idx(tj + u * TPC, slot);
@@ -1385,14 +1394,14 @@ __global__ void __launch_bounds__(ROWS * tpc_for<L>()) pass3_mid_kernel(Pass3Mid
   // W_{L2 L3}^{TPC k2} in between (as pass 2's twiddles)
   const uint32_t k1 = row / a.L2, k2 = row % a.L2;
   const float2* wc = a.tb.p2col + static_cast<size_t>(k1) * L;
-  auto wexact = [&](uint32_t e) { return cmul(a.tb.p2hi[e >> kP2LoBits], a.tb.p2lo[e & (kLo - 1)]); };
+  auto wexact = [&](uint32_t e) { return cmul(BRP_LD(&a.tb.p2hi[e >> kP2LoBits]), BRP_LD(&a.tb.p2lo[e & (kLo - 1)])); };
   const float2 step = wexact(static_cast<uint32_t>(TPC) * k2);
   float2 t = make_float2(1.f, 0.f);
 #pragma unroll
   for (int u = 0; u < kPer; ++u) {
     const uint32_t m3 = tj + u * TPC;
     if (u % 8 == 0) t = wexact(m3 * k2);
-    buf[rbase + m3] = cmul(data[Lay::idx(m3, slot)], cmul(wc[m3], t));
+    BRP_ST(&buf[rbase + m3], cmul(data[Lay::idx(m3, slot)], cmul(BRP_LD(&wc[m3]), t)));
     t = cmul(t, step);
   }
 }
@@ -1439,12 +1448,12 @@ hipError_t launch_pass1(const FFTPlan3& plan, Pass1Mode mode, const Pass1Args& a
   const bool pad3 = mode == P1_RESAMPLE && plan.L1 % 3 == 0 &&
                     2ull * (plan.L1 / 3) * a.L2L3 >= a.n_unpadded;
   if (pad3 && plan.L1 == 192) {
-    hipLaunchKernelGGL((pass1_pruned3_kernel<4>), grid, dim3(kNcol * 16), 0, s, a);
-    return hipGetLastError();
+    BRP_LAUNCH((pass1_pruned3_kernel<4>), grid, dim3(kNcol * 16), 0, s, a);
+    return launch_status();
   }
   if (pad3 && plan.L1 == 96) {
-    hipLaunchKernelGGL((pass1_pruned3_kernel<2>), grid, dim3(kNcol * 16), 0, s, a);
-    return hipGetLastError();
+    BRP_LAUNCH((pass1_pruned3_kernel<2>), grid, dim3(kNcol * 16), 0, s, a);
+    return launch_status();
   }
 #ifndef BRP_P1G
 #define BRP_P1G 1  // register-staged complex-input pass 1 (build switch)
@@ -1459,13 +1468,13 @@ hipError_t launch_pass1(const FFTPlan3& plan, Pass1Mode mode, const Pass1Args& a
 #define X(n)                                                                                                 \
   case n: {                                                                                                  \
     const dim3 blk(kNcol * (n / 16));                                                                        \
-    if (mode == P1_COMPLEX) hipLaunchKernelGGL((pass1g_kernel<n, P1_COMPLEX>), grid, blk, 0, s, a);          \
-    else if (mode == P1_COMPLEX_CONJ) hipLaunchKernelGGL((pass1g_kernel<n, P1_COMPLEX_CONJ>), grid, blk, 0, s, a); \
-    else if (mode == P1_CHIRP2) hipLaunchKernelGGL((pass1g_kernel<n, P1_CHIRP2>), grid, blk, 0, s, a);       \
-    else if (mode == P1_CHIRP1) hipLaunchKernelGGL((pass1g_kernel<n, P1_CHIRP1>), grid, blk, 0, s, a);       \
-    else if (mode == P1_REV_CHIRP) hipLaunchKernelGGL((pass1g_kernel<n, P1_REV_CHIRP>), grid, blk, 0, s, a); \
-    else hipLaunchKernelGGL((pass1g_kernel<n, P1_CHIRP1_PAIR>), grid, blk, 0, s, a);                         \
-    return hipGetLastError();                                                                                \
+    if (mode == P1_COMPLEX) BRP_LAUNCH((pass1g_kernel<n, P1_COMPLEX>), grid, blk, 0, s, a);          \
+    else if (mode == P1_COMPLEX_CONJ) BRP_LAUNCH((pass1g_kernel<n, P1_COMPLEX_CONJ>), grid, blk, 0, s, a); \
+    else if (mode == P1_CHIRP2) BRP_LAUNCH((pass1g_kernel<n, P1_CHIRP2>), grid, blk, 0, s, a);       \
+    else if (mode == P1_CHIRP1) BRP_LAUNCH((pass1g_kernel<n, P1_CHIRP1>), grid, blk, 0, s, a);       \
+    else if (mode == P1_REV_CHIRP) BRP_LAUNCH((pass1g_kernel<n, P1_REV_CHIRP>), grid, blk, 0, s, a); \
+    else BRP_LAUNCH((pass1g_kernel<n, P1_CHIRP1_PAIR>), grid, blk, 0, s, a);                         \
+    return launch_status();                                                                                \
   }
         X(48) X(64) X(80) X(128) X(256) X(384) X(512)
 #undef X
@@ -1476,14 +1485,14 @@ hipError_t launch_pass1(const FFTPlan3& plan, Pass1Mode mode, const Pass1Args& a
 #define X(n)                                                                                         \
   case n: {                                                                                          \
     const dim3 blk(kNcol * (n / 16));                                                                \
-    if (mode == P1_RESAMPLE) hipLaunchKernelGGL((pass1g_kernel<n, P1_RESAMPLE>), grid, blk, 0, s, a); \
-    else if (mode == P1_COMPLEX) hipLaunchKernelGGL((pass1g_kernel<n, P1_COMPLEX>), grid, blk, 0, s, a); \
-    else if (mode == P1_REV_CHIRP) hipLaunchKernelGGL((pass1g_kernel<n, P1_REV_CHIRP>), grid, blk, 0, s, a); \
-    else if (mode == P1_COMPLEX_CONJ) hipLaunchKernelGGL((pass1g_kernel<n, P1_COMPLEX_CONJ>), grid, blk, 0, s, a); \
-    else if (mode == P1_CHIRP2) hipLaunchKernelGGL((pass1g_kernel<n, P1_CHIRP2>), grid, blk, 0, s, a);             \
-    else if (mode == P1_CHIRP1) hipLaunchKernelGGL((pass1g_kernel<n, P1_CHIRP1>), grid, blk, 0, s, a);             \
-    else hipLaunchKernelGGL((pass1g_kernel<n, P1_CHIRP1_PAIR>), grid, blk, 0, s, a);                               \
-    return hipGetLastError();                                                                        \
+    if (mode == P1_RESAMPLE) BRP_LAUNCH((pass1g_kernel<n, P1_RESAMPLE>), grid, blk, 0, s, a); \
+    else if (mode == P1_COMPLEX) BRP_LAUNCH((pass1g_kernel<n, P1_COMPLEX>), grid, blk, 0, s, a); \
+    else if (mode == P1_REV_CHIRP) BRP_LAUNCH((pass1g_kernel<n, P1_REV_CHIRP>), grid, blk, 0, s, a); \
+    else if (mode == P1_COMPLEX_CONJ) BRP_LAUNCH((pass1g_kernel<n, P1_COMPLEX_CONJ>), grid, blk, 0, s, a); \
+    else if (mode == P1_CHIRP2) BRP_LAUNCH((pass1g_kernel<n, P1_CHIRP2>), grid, blk, 0, s, a);             \
+    else if (mode == P1_CHIRP1) BRP_LAUNCH((pass1g_kernel<n, P1_CHIRP1>), grid, blk, 0, s, a);             \
+    else BRP_LAUNCH((pass1g_kernel<n, P1_CHIRP1_PAIR>), grid, blk, 0, s, a);                               \
+    return launch_status();                                                                        \
   }
       X(96) X(112) X(144) X(160) X(192) X(224) X(240) X(288) X(320) X(448)
 #undef X
@@ -1494,20 +1503,20 @@ hipError_t launch_pass1(const FFTPlan3& plan, Pass1Mode mode, const Pass1Args& a
 #define X(n)                                                                                          \
   case n: {                                                                                           \
     const dim3 block(kNcol * tpc_for<n>());                                                           \
-    if (mode == P1_RESAMPLE) hipLaunchKernelGGL((pass1_kernel<n, P1_RESAMPLE>), grid, block, 0, s, a); \
-    else if (mode == P1_REAL) hipLaunchKernelGGL((pass1_kernel<n, P1_REAL>), grid, block, 0, s, a);    \
-    else if (mode == P1_COMPLEX) hipLaunchKernelGGL((pass1_kernel<n, P1_COMPLEX>), grid, block, 0, s, a); \
-    else if (mode == P1_CHIRP2) hipLaunchKernelGGL((pass1_kernel<n, P1_CHIRP2>), grid, block, 0, s, a);   \
-    else if (mode == P1_CHIRP1) hipLaunchKernelGGL((pass1_kernel<n, P1_CHIRP1>), grid, block, 0, s, a);   \
-    else if (mode == P1_CHIRP1_PAIR) hipLaunchKernelGGL((pass1_kernel<n, P1_CHIRP1_PAIR>), grid, block, 0, s, a); \
-    else hipLaunchKernelGGL((pass1_kernel<n, P1_COMPLEX_CONJ>), grid, block, 0, s, a);                 \
+    if (mode == P1_RESAMPLE) BRP_LAUNCH((pass1_kernel<n, P1_RESAMPLE>), grid, block, 0, s, a); \
+    else if (mode == P1_REAL) BRP_LAUNCH((pass1_kernel<n, P1_REAL>), grid, block, 0, s, a);    \
+    else if (mode == P1_COMPLEX) BRP_LAUNCH((pass1_kernel<n, P1_COMPLEX>), grid, block, 0, s, a); \
+    else if (mode == P1_CHIRP2) BRP_LAUNCH((pass1_kernel<n, P1_CHIRP2>), grid, block, 0, s, a);   \
+    else if (mode == P1_CHIRP1) BRP_LAUNCH((pass1_kernel<n, P1_CHIRP1>), grid, block, 0, s, a);   \
+    else if (mode == P1_CHIRP1_PAIR) BRP_LAUNCH((pass1_kernel<n, P1_CHIRP1_PAIR>), grid, block, 0, s, a); \
+    else BRP_LAUNCH((pass1_kernel<n, P1_COMPLEX_CONJ>), grid, block, 0, s, a);                 \
     break;                                                                                            \
   }
     BRP_P12_LENGTHS(X)
 #undef X
     default: return hipErrorInvalidValue;
   }
-  return hipGetLastError();
+  return launch_status();
 }
 
 hipError_t launch_pass2(const FFTPlan3& plan, const Pass2Args& a, int batch, hipStream_t s) {
@@ -1518,9 +1527,9 @@ hipError_t launch_pass2(const FFTPlan3& plan, const Pass2Args& a, int batch, hip
   switch (plan.L2) {
 #define X(n)                                                                                       \
   case n:                                                                                          \
-    if (a.rev) hipLaunchKernelGGL((pass2r_kernel<n, true>), grid, dim3(kNcol * (n / 16)), 0, s, a, ntiles); \
-    else hipLaunchKernelGGL((pass2r_kernel<n>), grid, dim3(kNcol * (n / 16)), 0, s, a, ntiles);   \
-    return hipGetLastError();
+    if (a.rev) BRP_LAUNCH((pass2r_kernel<n, true>), grid, dim3(kNcol * (n / 16)), 0, s, a, ntiles); \
+    else BRP_LAUNCH((pass2r_kernel<n>), grid, dim3(kNcol * (n / 16)), 0, s, a, ntiles);   \
+    return launch_status();
     BRP_P2R_LENGTHS(X)
 #undef X
     default: break;
@@ -1534,9 +1543,9 @@ hipError_t launch_pass2(const FFTPlan3& plan, const Pass2Args& a, int batch, hip
     switch (plan.L2) {
 #define X(n)                                                                                       \
   case n:                                                                                          \
-    if (a.rev) hipLaunchKernelGGL((pass2g_kernel<n, true>), grid, dim3(kNcol * (n / 16)), 0, s, a, ntiles); \
-    else hipLaunchKernelGGL((pass2g_kernel<n>), grid, dim3(kNcol * (n / 16)), 0, s, a, ntiles);   \
-    return hipGetLastError();
+    if (a.rev) BRP_LAUNCH((pass2g_kernel<n, true>), grid, dim3(kNcol * (n / 16)), 0, s, a, ntiles); \
+    else BRP_LAUNCH((pass2g_kernel<n>), grid, dim3(kNcol * (n / 16)), 0, s, a, ntiles);   \
+    return launch_status();
       BRP_P2G_LENGTHS(X)
 #undef X
       default: break;
@@ -1546,13 +1555,13 @@ hipError_t launch_pass2(const FFTPlan3& plan, const Pass2Args& a, int batch, hip
   switch (plan.L2) {
 #define X(n)                                                                \
   case n:                                                                   \
-    hipLaunchKernelGGL((pass2_kernel<n>), grid, dim3(kNcol * tpc_for<n>()), 0, s, a, ntiles); \
+    BRP_LAUNCH((pass2_kernel<n>), grid, dim3(kNcol * tpc_for<n>()), 0, s, a, ntiles); \
     break;
     BRP_P12_LENGTHS(X)
 #undef X
     default: return hipErrorInvalidValue;
   }
-  return hipGetLastError();
+  return launch_status();
 }
 
 constexpr int kRows3 = 8;
@@ -1570,16 +1579,16 @@ hipError_t launch_pass3(const FFTPlan3& plan, Pass3Mode mode, const Pass3Args& a
   case n: {                                                                                               \
     const dim3 block(2 * kRowsP * tpc_for<n>());                                                          \
     if (mode == P3_POWER && a.ps16)                                                                       \
-      hipLaunchKernelGGL((pass3_kernel<n, kRowsP, P3_POWER16>), grid, block, 0, s, a);                    \
-    else if (mode == P3_POWER) hipLaunchKernelGGL((pass3_kernel<n, kRowsP, P3_POWER>), grid, block, 0, s, a); \
-    else hipLaunchKernelGGL((pass3_kernel<n, kRowsP, P3_COMPLEX>), grid, block, 0, s, a);                 \
+      BRP_LAUNCH((pass3_kernel<n, kRowsP, P3_POWER16>), grid, block, 0, s, a);                    \
+    else if (mode == P3_POWER) BRP_LAUNCH((pass3_kernel<n, kRowsP, P3_POWER>), grid, block, 0, s, a); \
+    else BRP_LAUNCH((pass3_kernel<n, kRowsP, P3_COMPLEX>), grid, block, 0, s, a);                 \
     break;                                                                                                \
   }
     BRP_P3_LENGTHS(X)
 #undef X
     default: return hipErrorInvalidValue;
   }
-  return hipGetLastError();
+  return launch_status();
 }
 
 hipError_t launch_pass3_cplx(const FFTPlan3& plan, Pass3CplxMode mode, const Pass3CplxArgs& a, int batch,
@@ -1589,16 +1598,16 @@ hipError_t launch_pass3_cplx(const FFTPlan3& plan, Pass3CplxMode mode, const Pas
 #define X(n)                                                                                                       \
   case n: {                                                                                                        \
     const dim3 block(kRows3 * tpc_for<n>());                                                                       \
-    if (mode == C3_PLAIN) hipLaunchKernelGGL((pass3_cplx_kernel<n, kRows3, C3_PLAIN>), grid, block, 0, s, a);     \
-    else if (mode == C3_MULCONJ) hipLaunchKernelGGL((pass3_cplx_kernel<n, kRows3, C3_MULCONJ>), grid, block, 0, s, a); \
-    else hipLaunchKernelGGL((pass3_cplx_kernel<n, kRows3, C3_CHIRP>), grid, block, 0, s, a);                     \
+    if (mode == C3_PLAIN) BRP_LAUNCH((pass3_cplx_kernel<n, kRows3, C3_PLAIN>), grid, block, 0, s, a);     \
+    else if (mode == C3_MULCONJ) BRP_LAUNCH((pass3_cplx_kernel<n, kRows3, C3_MULCONJ>), grid, block, 0, s, a); \
+    else BRP_LAUNCH((pass3_cplx_kernel<n, kRows3, C3_CHIRP>), grid, block, 0, s, a);                     \
     break;                                                                                                         \
   }
     BRP_P3_LENGTHS(X)
 #undef X
     default: return hipErrorInvalidValue;
   }
-  return hipGetLastError();
+  return launch_status();
 }
 
 bool chirp_rev_supported(const FFTPlan3& plan) {
@@ -1644,10 +1653,10 @@ hipError_t launch_pass3_mid(const FFTPlan3& plan, const Pass3MidArgs& a, int bat
     constexpr int R = mid_rows<n>();                                                                      \
     if (!a.whole_waves || R == 8) {                                                                       \
       if (rows % 8 != 0) return hipErrorInvalidValue;                                                     \
-      hipLaunchKernelGGL((pass3_mid_kernel<n, 8>), dim3(rows / 8, batch), dim3(8 * tpc_for<n>()), 0, s, a); \
+      BRP_LAUNCH((pass3_mid_kernel<n, 8>), dim3(rows / 8, batch), dim3(8 * tpc_for<n>()), 0, s, a); \
     } else {                                                                                              \
       if (rows % R != 0) return hipErrorInvalidValue;                                                     \
-      hipLaunchKernelGGL((pass3_mid_kernel<n, R>), dim3(rows / R, batch), dim3(R * tpc_for<n>()), 0, s, a); \
+      BRP_LAUNCH((pass3_mid_kernel<n, R>), dim3(rows / R, batch), dim3(R * tpc_for<n>()), 0, s, a); \
     }                                                                                                     \
     break;                                                                                                \
   }
@@ -1655,7 +1664,7 @@ hipError_t launch_pass3_mid(const FFTPlan3& plan, const Pass3MidArgs& a, int bat
 #undef X
     default: return hipErrorInvalidValue;
   }
-  return hipGetLastError();
+  return launch_status();
 }
 
 hipError_t launch_pass3_plain(const FFTPlan3& plan, const Pass3PlainArgs& a, hipStream_t s) {
@@ -1663,13 +1672,13 @@ hipError_t launch_pass3_plain(const FFTPlan3& plan, const Pass3PlainArgs& a, hip
   switch (plan.L3) {
 #define X(n)                                                                                       \
   case n:                                                                                          \
-    hipLaunchKernelGGL((pass3_plain_kernel<n, kRows3>), grid, dim3(kRows3 * tpc_for<n>()), 0, s, a); \
+    BRP_LAUNCH((pass3_plain_kernel<n, kRows3>), grid, dim3(kRows3 * tpc_for<n>()), 0, s, a); \
     break;
     BRP_P3_LENGTHS(X)
 #undef X
     default: return hipErrorInvalidValue;
   }
-  return hipGetLastError();
+  return launch_status();
 }
 
 }  // namespace hipk

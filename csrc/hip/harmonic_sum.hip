@@ -36,12 +36,12 @@ __device__ __forceinline__ void emit(uint32_t* counter, uint2* list, uint32_t ca
   const int lane = threadIdx.x % kWave;
   const int leader = __ffsll(static_cast<long long>(mask)) - 1;
   uint32_t base = 0;
-  if (lane == leader) base = atomicAdd(counter, static_cast<uint32_t>(__popcll(mask)));
+  if (lane == leader && BRP_CHK(counter, sizeof(uint32_t))) base = atomicAdd(counter, static_cast<uint32_t>(__popcll(mask)));
   base = __shfl(base, leader, kWave);
   if (pred) {
     const uint32_t rank = __popcll(mask & ((1ull << lane) - 1ull));
     const uint32_t slot = base + rank;
-    if (slot < cap) list[slot] = make_uint2(key, __float_as_uint(power));
+    if (slot < cap) BRP_ST(&list[slot], make_uint2(key, __float_as_uint(power)));
   }
 }
 
@@ -84,6 +84,9 @@ __global__ void __launch_bounds__(kThreads) harmonic_sum_kernel(HSArgs a) {
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
       kHalf ? static_cast<void*>(const_cast<_Float16*>(P16)) : static_cast<void*>(const_cast<float*>(P32)), 0,
       static_cast<int>(a.ps_stride * kEsz), 0x00020000);
+  // the descriptor's whole range lies in the spectrum allocation
+  if (threadIdx.x == 0)
+    (void)BRP_CHK(kHalf ? static_cast<const void*>(P16) : static_cast<const void*>(P32), a.ps_stride * kEsz);
   const int ib = i0 + static_cast<int>(threadIdx.x);
   uint32_t off[17];
 #pragma unroll
@@ -133,7 +136,7 @@ __global__ void __launch_bounds__(kThreads) harmonic_sum_kernel(HSArgs a) {
 
   uint32_t* count = &a.list[0].x;
   uint2* list = a.list + 1;
-  const float thr0 = a.thr[static_cast<size_t>(b) * kHsThrStride + 0];
+  const float thr0 = BRP_LD(&a.thr[static_cast<size_t>(b) * kHsThrStride + 0]);
   // level 0: the power spectrum itself (kept in registers from the S_1 sums)
 #pragma unroll
   for (int it = 0; it < kIt; ++it) {
@@ -143,7 +146,7 @@ __global__ void __launch_bounds__(kThreads) harmonic_sum_kernel(HSArgs a) {
     const bool in = t < TILE && (i >= w2 && i < fhi);
     const float p = in ? p0[it] : 0.0f;
     if constexpr (DENSE) {
-      if (in) a.dense[(static_cast<size_t>(b) * 5 + 0) * a.dense_stride + i] = p > thr0 ? p : 0.0f;
+      if (in) BRP_ST(&a.dense[(static_cast<size_t>(b) * 5 + 0) * a.dense_stride + i], p > thr0 ? p : 0.0f);
     } else {
       emit(count, list, a.cap, in && p > thr0, hs_pack(a.key_base + b, 0, static_cast<uint32_t>(i), a.bin_bits), p);
     }
@@ -155,7 +158,7 @@ __global__ void __launch_bounds__(kThreads) harmonic_sum_kernel(HSArgs a) {
   for (int h = 1; h <= 4; ++h) {
     const int g = 1 << h;
     const int off = g >> 1;
-    const float thr = a.thr[static_cast<size_t>(b) * kHsThrStride + h];
+    const float thr = BRP_LD(&a.thr[static_cast<size_t>(b) * kHsThrStride + h]);
     const int first = static_cast<int>((off - (i0 % g) + g) % g);
     const int ngroups = (TILE - first + g - 1) / g;
     for (int q = threadIdx.x; q < ((ngroups + kThreads - 1) / kThreads) * kThreads; q += kThreads) {
@@ -174,7 +177,7 @@ __global__ void __launch_bounds__(kThreads) harmonic_sum_kernel(HSArgs a) {
         }
       }
       if constexpr (DENSE) {
-        if (inr) a.dense[(static_cast<size_t>(b) * 5 + h) * a.dense_stride + j] = pred ? m : 0.0f;
+        if (inr) BRP_ST(&a.dense[(static_cast<size_t>(b) * 5 + h) * a.dense_stride + j], pred ? m : 0.0f);
       } else {
         emit(count, list, a.cap, pred, hs_pack(a.key_base + b, h, static_cast<uint32_t>(j), a.bin_bits), m);
       }
@@ -224,13 +227,13 @@ __global__ void __launch_bounds__(256) hs_cells_kernel(HSArgs a) {
     if constexpr (MODE == HS_F32) {
 #pragma unroll
       for (int e = 0; e < W / 4; ++e) {
-        const float4 x = reinterpret_cast<const float4*>(P + k0)[e];
+        const float4 x = BRP_LD(&reinterpret_cast<const float4*>(P + k0)[e]);
         v[4 * e] = x.x; v[4 * e + 1] = x.y; v[4 * e + 2] = x.z; v[4 * e + 3] = x.w;
       }
     } else {
 #pragma unroll
       for (int e = 0; e < W / 4; ++e) {  // 4 halves per 8-byte load
-        const uint2 x = reinterpret_cast<const uint2*>(P + k0)[e];
+        const uint2 x = BRP_LD(&reinterpret_cast<const uint2*>(P + k0)[e]);
         const uint32_t w[2] = {x.x, x.y};
 #pragma unroll
         for (int q = 0; q < 4; ++q)
@@ -241,13 +244,15 @@ __global__ void __launch_bounds__(256) hs_cells_kernel(HSArgs a) {
   } else {
 #pragma unroll
     for (int e = 0; e < W; ++e)  // never read by the exact sums
-      v[e] = (k0 + e < a.hhi) ? static_cast<float>(P[k0 + e]) : 0.0f;
+      v[e] = (k0 + e < a.hhi) ? static_cast<float>(BRP_LD(&P[k0 + e])) : 0.0f;
   }
 #pragma unroll
   for (int w = W / 2; w >= 1; w /= 2)
 #pragma unroll
     for (int e = 0; e < w; ++e) v[e] = fmaxf(v[e], v[e + w]);
-  a.pyr[static_cast<size_t>(b) * a.pyr_stride + m] = v[0];
+  BRP_ST(&a.pyr[BRP_INJECT_AT(static_cast<size_t>(b) * a.pyr_stride + m, static_cast<size_t>(gridDim.y) * a.pyr_stride + 16,
+                               kInjHsCells)],
+         v[0]);
 }
 
 // harmonics in the reference summation order, their source (0: spectrum,
@@ -293,7 +298,7 @@ __device__ __forceinline__ void hs_load(float* v, const T* P, const float* C8, u
 #pragma unroll
   for (int q = 0; q < S::chunks(Q); ++q) {
     const uint32_t c = c0 + static_cast<uint32_t>(lane + kWave * q);
-    const float x = K ? C8[min(c, lim - 1)] : static_cast<float>(P[min(c, lim - 1)]);
+    const float x = K ? BRP_LD(&C8[min(c, lim - 1)]) : static_cast<float>(BRP_LD(&P[min(c, lim - 1)]));
     v[S::chunk0(Q) + q] = c < lim ? x : 0.0f;
   }
 }
@@ -437,15 +442,15 @@ __device__ __forceinline__ f4u hs_direct_load(const PsT<MODE>* P, const float* C
   if constexpr (H::K > 0 || MODE == HS_F32) {
     const float* src = (H::K > 0 ? C8 : reinterpret_cast<const float*>(P)) + lo;
     if constexpr (H::kN == 1) {
-      v.x = *src;
+      v.x = BRP_LD(src);
     } else {
-      const fvu<H::kN> w = *reinterpret_cast<const fvu<H::kN>*>(src);
+      const fvu<H::kN> w = BRP_LD(reinterpret_cast<const fvu<H::kN>*>(src));
 #pragma unroll
       for (int e = 0; e < H::kN; ++e) v[e] = w[e];
     }
   } else {
 #pragma unroll
-    for (int e = 0; e < H::kN; ++e) v[e] = static_cast<float>(P[lo + e]);
+    for (int e = 0; e < H::kN; ++e) v[e] = static_cast<float>(BRP_LD(&P[lo + e]));
   }
   return v;
 }
@@ -605,7 +610,8 @@ __global__ void __launch_bounds__(256) hs_pruned_kernel(HSArgs a, uint32_t nblk)
   const int w2 = static_cast<int>(a.w2), fhi = static_cast<int>(a.fhi), hhi = static_cast<int>(a.hhi);
   const int32_t I0 = a.i_start + static_cast<int32_t>(kBlk * wave_blk0);
   float* buf = stage[DIRECT ? 0 : wave];
-  const float* C8 = a.pyr + static_cast<size_t>(b) * a.pyr_stride;
+  const float* C8 = a.pyr + BRP_INJECT_AT(static_cast<size_t>(b) * a.pyr_stride,
+                                          static_cast<size_t>(gridDim.y) * a.pyr_stride + 16, kInjHsPruned);
   if constexpr (!DIRECT) hs_stage_all<CK>(std::make_integer_sequence<int, 16>{}, buf, P, C8, a.pyr_stride, a.ps_stride, I0, lane);
   // LDS operations of one wave complete in order; keep the compiler from moving them
   auto wave_sync = [] {
@@ -623,7 +629,7 @@ __global__ void __launch_bounds__(256) hs_pruned_kernel(HSArgs a, uint32_t nblk)
   // per level after the bounds
   float th[5];
 #pragma unroll
-  for (int h = 0; h <= 4; ++h) th[h] = thr[h];
+  for (int h = 0; h <= 4; ++h) th[h] = BRP_LD(&thr[h]);
   if (blk < nblk) {
     const int32_t ib = I0 + kBlk * lane;
     float u[5];
@@ -661,7 +667,7 @@ __global__ void __launch_bounds__(256) hs_pruned_kernel(HSArgs a, uint32_t nblk)
     const int i = ib + li;
     float s1 = ninf, s2 = ninf, s3 = ninf, s4 = ninf, p0 = 0.0f;
     if (act && i >= w2 && i < hhi) {
-      auto ld = [&](int l) { return static_cast<float>(P[(l * i + 8) >> 4]); };
+      auto ld = [&](int l) { return static_cast<float>(BRP_LD(&P[(l * i + 8) >> 4])); };
       float sum = ld(16);
       p0 = sum;
       sum += ld(8);
@@ -722,6 +728,7 @@ __global__ void __launch_bounds__(256) hs_sel_hist_kernel(HSArgs a, HsSelectArgs
   const uint32_t h = blockIdx.y, b = blockIdx.z;
   const size_t row = static_cast<size_t>(b) * 5 + h;
   const uint32_t* st = s.state + row * 4;
+  if (threadIdx.x == 0) (void)BRP_CHK(st, 4 * sizeof(uint32_t));
   if (ROUND > 0 && st[2] != 0) return;  // uniform: fewer than K values, nothing to refine
   for (uint32_t e = threadIdx.x; e < (1u << kBits); e += 256) hist[e] = 0;
   __syncthreads();
@@ -729,7 +736,7 @@ __global__ void __launch_bounds__(256) hs_sel_hist_kernel(HSArgs a, HsSelectArgs
   const uint32_t* v = reinterpret_cast<const uint32_t*>(s.dense) + row * s.dense_stride;
   const uint32_t lo = a.w2 + blockIdx.x * kSelChunk, hi = min(lo + kSelChunk, a.fhi);
   for (uint32_t j = lo + threadIdx.x; j < hi; j += 256) {
-    const uint32_t u = v[j];
+    const uint32_t u = BRP_LD(&v[j]);
     if (u == 0 || (u >> 31) != 0) continue;  // not above threshold
     if (ROUND > 0 && (u >> (kShift + kBits)) != (prefix >> (kShift + kBits))) continue;
     atomicAdd(&hist[(u >> kShift) & ((1u << kBits) - 1u)], 1u);
@@ -737,7 +744,7 @@ __global__ void __launch_bounds__(256) hs_sel_hist_kernel(HSArgs a, HsSelectArgs
   __syncthreads();
   uint32_t* g = s.hist + row * kHsSelBins;
   for (uint32_t e = threadIdx.x; e < (1u << kBits); e += 256)
-    if (hist[e] != 0) atomicAdd(&g[e], hist[e]);
+    if (hist[e] != 0 && BRP_CHK(&g[e], sizeof(uint32_t))) atomicAdd(&g[e], hist[e]);
 }
 
 // one wave per (template, level): lane l owns bins [32 l, 32 l + 32)
@@ -748,6 +755,7 @@ __global__ void __launch_bounds__(64) hs_sel_pick_kernel(HSArgs a, HsSelectArgs 
   const uint32_t h = blockIdx.x, b = blockIdx.y;
   const size_t row = static_cast<size_t>(b) * 5 + h;
   uint32_t* st = s.state + row * 4;
+  if (threadIdx.x == 0) (void)BRP_CHK(st, 4 * sizeof(uint32_t));
   uint32_t* g = s.hist + row * kHsSelBins;
   const int lane = threadIdx.x;
   if (ROUND > 0 && st[2] != 0) return;
@@ -755,8 +763,8 @@ __global__ void __launch_bounds__(64) hs_sel_pick_kernel(HSArgs a, HsSelectArgs 
   uint32_t sum = 0;
 #pragma unroll
   for (int e = 0; e < kPer; ++e) {
-    mine[e] = g[lane * kPer + e];
-    g[lane * kPer + e] = 0;  // cleared for the next round
+    mine[e] = BRP_LD(&g[lane * kPer + e]);
+    BRP_ST(&g[lane * kPer + e], 0u);  // cleared for the next round
     sum += mine[e];
   }
   // suffix sums over the lanes: values in the bins of lanes >= lane
@@ -771,7 +779,7 @@ __global__ void __launch_bounds__(64) hs_sel_pick_kernel(HSArgs a, HsSelectArgs 
   if (ROUND == 0) {
     if (lane == 0) {
       st[3] = total;
-      atomicAdd(&a.list[0].y, total);
+      if (BRP_CHK(&a.list[0].y, sizeof(uint32_t))) atomicAdd(&a.list[0].y, total);
     }
     if (total < krem) {  // fewer than K values above threshold: all of them are kept
       if (lane == 0) st[2] = 1;
@@ -798,7 +806,7 @@ __global__ void __launch_bounds__(64) hs_sel_pick_kernel(HSArgs a, HsSelectArgs 
 
 __global__ void hs_sel_init_kernel(uint32_t* state, uint32_t rows, uint32_t k) {
   const uint32_t r = blockIdx.x * 256u + threadIdx.x;
-  if (r < rows) reinterpret_cast<uint4*>(state)[r] = make_uint4(0u, k, 0u, 0u);
+  if (r < rows) BRP_ST(&reinterpret_cast<uint4*>(state)[r], make_uint4(0u, k, 0u, 0u));
 }
 
 // emit every value >= the K-th largest (all of them when there are fewer than K)
@@ -806,6 +814,7 @@ __global__ void __launch_bounds__(256) hs_sel_emit_kernel(HSArgs a, HsSelectArgs
   const uint32_t h = blockIdx.y, b = blockIdx.z;
   const size_t row = static_cast<size_t>(b) * 5 + h;
   const uint32_t* st = s.state + row * 4;
+  if (threadIdx.x == 0) (void)BRP_CHK(st, 4 * sizeof(uint32_t));
   const uint32_t kth = st[2] != 0 ? 1u : st[0];
   const uint32_t* v = reinterpret_cast<const uint32_t*>(s.dense) + row * s.dense_stride;
   const uint32_t lo = a.w2 + blockIdx.x * kSelChunk, hi = min(lo + kSelChunk, a.fhi);
@@ -814,7 +823,7 @@ __global__ void __launch_bounds__(256) hs_sel_emit_kernel(HSArgs a, HsSelectArgs
   // whole-wave iterations (emit aggregates with a ballot)
   for (uint32_t j0 = lo; j0 < hi; j0 += 256) {
     const uint32_t j = j0 + threadIdx.x;
-    const uint32_t u = j < hi ? v[j] : 0u;
+    const uint32_t u = j < hi ? BRP_LD(&v[j]) : 0u;
     const bool keep = u != 0 && (u >> 31) == 0 && u >= kth;
     emit(count, list, a.cap, keep, hs_pack(a.key_base + b, h, j, a.bin_bits), __uint_as_float(u));
   }
@@ -841,8 +850,8 @@ hipError_t launch_harmonic_sum(const HSArgs& a, int batch, hipStream_t s) {
     const dim3 gc((hs_pyr_stride(a.ps_stride) + 255) / 256, batch), gp((nblk + 255) / 256, batch);
 #define BRP_HS_PRUNED(CK, MODE, DIRECT)                                              \
   do {                                                                              \
-    hipLaunchKernelGGL((hs_cells_kernel<CK, MODE>), gc, dim3(256), 0, s, a);         \
-    hipLaunchKernelGGL((hs_pruned_kernel<CK, MODE, DIRECT>), gp, dim3(256), 0, s, a, nblk); \
+    BRP_LAUNCH((hs_cells_kernel<CK, MODE>), gc, dim3(256), 0, s, a);         \
+    BRP_LAUNCH((hs_pruned_kernel<CK, MODE, DIRECT>), gp, dim3(256), 0, s, a, nblk); \
   } while (0)
     if (a.mode == HS_F16) {
       if (a.cell_shift == 2) BRP_HS_PRUNED(2, HS_F16, false);
@@ -854,16 +863,16 @@ hipError_t launch_harmonic_sum(const HSArgs& a, int batch, hipStream_t s) {
       else BRP_HS_PRUNED(3, HS_F32, false);
     }
 #undef BRP_HS_PRUNED
-    return hipGetLastError();
+    return launch_status();
   }
   const uint32_t tiles = hs_num_tiles(a.i_start, a.hhi);
   if (tiles == 0) return hipSuccess;
   const dim3 grid(tiles, batch);
   switch (a.mode) {
-    case HS_F16: hipLaunchKernelGGL(harmonic_sum_kernel<HS_F16>, grid, dim3(kThreads), 0, s, a); break;
-    default: hipLaunchKernelGGL(harmonic_sum_kernel<HS_F32>, grid, dim3(kThreads), 0, s, a); break;
+    case HS_F16: BRP_LAUNCH(harmonic_sum_kernel<HS_F16>, grid, dim3(kThreads), 0, s, a); break;
+    default: BRP_LAUNCH(harmonic_sum_kernel<HS_F32>, grid, dim3(kThreads), 0, s, a); break;
   }
-  return hipGetLastError();
+  return launch_status();
 }
 
 
@@ -878,19 +887,19 @@ hipError_t launch_harmonic_sum_select(const HSArgs& a0, const HsSelectArgs& s, i
   if ((e = hipMemsetAsync(s.dense, 0, rows * s.dense_stride * sizeof(float), st)) != hipSuccess) return e;
   if ((e = hipMemsetAsync(s.hist, 0, rows * kHsSelBins * sizeof(uint32_t), st)) != hipSuccess) return e;
   const dim3 grid(tiles, batch);
-  if (a.mode == HS_F16) hipLaunchKernelGGL((harmonic_sum_kernel<HS_F16, true>), grid, dim3(kThreads), 0, st, a);
-  else hipLaunchKernelGGL((harmonic_sum_kernel<HS_F32, true>), grid, dim3(kThreads), 0, st, a);
+  if (a.mode == HS_F16) BRP_LAUNCH((harmonic_sum_kernel<HS_F16, true>), grid, dim3(kThreads), 0, st, a);
+  else BRP_LAUNCH((harmonic_sum_kernel<HS_F32, true>), grid, dim3(kThreads), 0, st, a);
   const dim3 gh((a.fhi - a.w2 + kSelChunk - 1) / kSelChunk, 5, batch), gp(5, batch);
-  hipLaunchKernelGGL(hs_sel_init_kernel, dim3((rows + 255) / 256), dim3(256), 0, st, s.state,
+  BRP_LAUNCH(hs_sel_init_kernel, dim3((rows + 255) / 256), dim3(256), 0, st, s.state,
                      static_cast<uint32_t>(rows), s.k);
-  hipLaunchKernelGGL(hs_sel_hist_kernel<0>, gh, dim3(256), 0, st, a, s);
-  hipLaunchKernelGGL(hs_sel_pick_kernel<0>, gp, dim3(64), 0, st, a, s);
-  hipLaunchKernelGGL(hs_sel_hist_kernel<1>, gh, dim3(256), 0, st, a, s);
-  hipLaunchKernelGGL(hs_sel_pick_kernel<1>, gp, dim3(64), 0, st, a, s);
-  hipLaunchKernelGGL(hs_sel_hist_kernel<2>, gh, dim3(256), 0, st, a, s);
-  hipLaunchKernelGGL(hs_sel_pick_kernel<2>, gp, dim3(64), 0, st, a, s);
-  hipLaunchKernelGGL(hs_sel_emit_kernel, gh, dim3(256), 0, st, a, s);
-  return hipGetLastError();
+  BRP_LAUNCH(hs_sel_hist_kernel<0>, gh, dim3(256), 0, st, a, s);
+  BRP_LAUNCH(hs_sel_pick_kernel<0>, gp, dim3(64), 0, st, a, s);
+  BRP_LAUNCH(hs_sel_hist_kernel<1>, gh, dim3(256), 0, st, a, s);
+  BRP_LAUNCH(hs_sel_pick_kernel<1>, gp, dim3(64), 0, st, a, s);
+  BRP_LAUNCH(hs_sel_hist_kernel<2>, gh, dim3(256), 0, st, a, s);
+  BRP_LAUNCH(hs_sel_pick_kernel<2>, gp, dim3(64), 0, st, a, s);
+  BRP_LAUNCH(hs_sel_emit_kernel, gh, dim3(256), 0, st, a, s);
+  return launch_status();
 }
 
 }  // namespace hipk

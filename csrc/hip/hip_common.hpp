@@ -8,6 +8,7 @@
 
 #include "../core/errors.hpp"
 #include "../core/log.hpp"
+#include "checked.hpp"
 
 namespace brp {
 namespace hipk {
@@ -98,14 +99,14 @@ __device__ __forceinline__ uint32_t mod_u64(uint64_t j, uint32_t m, double inv_m
 __device__ __forceinline__ float2 tw_lookup(const TwiddleTable& t, uint64_t j) {
   if (t.inv_period != 0.0 && j < (1ull << 60)) j = mod_u64(j, static_cast<uint32_t>(t.period), t.inv_period);
   else j %= t.period;
-  const float2 a = t.hi[j >> kTwLoBits];
-  const float2 b = t.lo[j & ((1u << kTwLoBits) - 1)];
+  const float2 a = BRP_LD(&t.hi[j >> kTwLoBits]);
+  const float2 b = BRP_LD(&t.lo[j & ((1u << kTwLoBits) - 1)]);
   return cmul(a, b);
 }
 // same for an exponent already known to be < period (32-bit fast path)
 __device__ __forceinline__ float2 tw_lookup32(const TwiddleTable& t, uint32_t j) {
-  const float2 a = t.hi[j >> kTwLoBits];
-  const float2 b = t.lo[j & ((1u << kTwLoBits) - 1)];
+  const float2 a = BRP_LD(&t.hi[j >> kTwLoBits]);
+  const float2 b = BRP_LD(&t.lo[j & ((1u << kTwLoBits) - 1)]);
   return cmul(a, b);
 }
 
@@ -119,11 +120,20 @@ __device__ __forceinline__ uint32_t xcd_remap(uint32_t bid, uint32_t nwg) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
 }
 
-// wave-level maximum (64 lanes) of a uint32, uniform result
+// maximum over the wave's active lanes of a value below 2^BITS, uniform
+// result: one ballot per bit from the top. A partial last wave (workgroups of
+// 48 / 80 / 112 threads) has inactive lanes, and a cross-lane shuffle would
+// read their stale registers; a ballot only counts lanes that run.
+template <int BITS>
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+  static_assert(BITS >= 1 && BITS <= 32, "value bits");
+  uint32_t m = 0;
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v = max(v, static_cast<uint32_t>(__shfl_xor(static_cast<int>(v), off, 64)));
-  return __builtin_amdgcn_readfirstlane(v);
+  for (int bit = BITS - 1; bit >= 0; --bit) {
+    const uint32_t c = m | (1u << bit);
+    if (__ballot(v >= c) != 0) m = c;
+  }
+  return __builtin_amdgcn_readfirstlane(m);
 }
 
 // wave-level sum (64 lanes) of a double

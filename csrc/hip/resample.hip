@@ -18,9 +18,9 @@ constexpr int kThreads = 256;
 
 __global__ void __launch_bounds__(kThreads) nsteps_kernel(TemplateDev* tmpl, uint32_t* reset) {
   __shared__ uint32_t best;
-  if (reset != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *reset = 0;
+  if (reset != nullptr && blockIdx.x == 0 && threadIdx.x == 0) BRP_ST(reset, 0u);
   TemplateDev& td = tmpl[blockIdx.x];
-  const ResampParams p = td.p;
+  const ResampParams p = BRP_LD(&td).p;
   const uint32_t nu = p.nsamples_unpadded;
   // |del_t| <= |tau*step_inv| + |S0| (+ LUT error); scan that tail plus margin
   const float reach = fabsf(p.tau * p.step_inv) + fabsf(p.S0) + 4.0f;
@@ -40,36 +40,36 @@ __global__ void __launch_bounds__(kThreads) nsteps_kernel(TemplateDev* tmpl, uin
   }
   if (found) atomicMax(&best, local);
   __syncthreads();
-  if (threadIdx.x == 0) td.n_steps = best;
+  if (threadIdx.x == 0) BRP_ST(&td.n_steps, best);
 }
 
 __global__ void resample_kernel(const float* series, uint32_t n_unpadded, const TemplateDev* tmpl, float* out,
                                 uint32_t nsamples) {
   const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= nsamples) return;
-  const TemplateDev td = *tmpl;
+  const TemplateDev td = BRP_LD(tmpl);
   float v = 0.0f;
   if (m < td.n_steps) {
     const float d = resamp_del_t(m, td.p, kSinLut, kCosLut);
     int idx = resamp_nearest(m, d);
     idx = idx < 0 ? 0 : (idx >= static_cast<int>(n_unpadded) ? static_cast<int>(n_unpadded) - 1 : idx);
-    v = series[idx];
+    v = BRP_LD(&series[idx]);
   }
-  out[m] = v;
+  BRP_ST(&out[m], v);
 }
 
 }  // namespace
 
 hipError_t launch_nsteps(TemplateDev* tmpl, int batch, hipStream_t s, uint32_t* reset) {
-  hipLaunchKernelGGL(nsteps_kernel, dim3(batch), dim3(kThreads), 0, s, tmpl, reset);
-  return hipGetLastError();
+  BRP_LAUNCH(nsteps_kernel, dim3(batch), dim3(kThreads), 0, s, tmpl, reset);
+  return launch_status();
 }
 
 hipError_t launch_resample(const float* series, uint32_t n_unpadded, const TemplateDev* tmpl, float* out,
                            uint32_t nsamples, hipStream_t s) {
-  hipLaunchKernelGGL(resample_kernel, dim3((nsamples + 255) / 256), dim3(256), 0, s, series, n_unpadded, tmpl, out,
+  BRP_LAUNCH(resample_kernel, dim3((nsamples + 255) / 256), dim3(256), 0, s, series, n_unpadded, tmpl, out,
                      nsamples);
-  return hipGetLastError();
+  return launch_status();
 }
 
 }  // namespace hipk

@@ -41,8 +41,8 @@ __device__ __forceinline__ uint32_t sort_key(float f) {
 __global__ void __launch_bounds__(kRsThreads) rs_init(const float* in, uint32_t n, uint32_t* keys, uint32_t* vals) {
   const uint32_t i = blockIdx.x * kRsThreads + threadIdx.x;
   if (i >= n) return;
-  keys[i] = sort_key(in[i]);
-  vals[i] = i;
+  BRP_ST(&keys[i], sort_key(BRP_LD(&in[i])));
+  BRP_ST(&vals[i], i);
 }
 
 // digit histogram of one tile; hist is digit-major: hist[d * nblocks + block]
@@ -55,10 +55,10 @@ __global__ void __launch_bounds__(kRsThreads) rs_hist(const uint32_t* keys, uint
 #pragma unroll 4
   for (int r = 0; r < kRsPer; ++r) {
     const uint32_t i = b0 + r * kRsThreads + threadIdx.x;
-    if (i < n) atomicAdd(&h[(keys[i] >> shift) & 255u], 1u);
+    if (i < n) atomicAdd(&h[(BRP_LD(&keys[i]) >> shift) & 255u], 1u);
   }
   __syncthreads();
-  hist[threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
+  BRP_ST(&hist[threadIdx.x * nblocks + blockIdx.x], h[threadIdx.x]);
 }
 
 // exclusive scan of hist[0 .. total) in place, one workgroup
@@ -67,7 +67,7 @@ __global__ void __launch_bounds__(1024) rs_scan(uint32_t* hist, uint32_t total) 
   const uint32_t per = (total + 1023) / 1024;
   const uint32_t lo = threadIdx.x * per, hi = min(lo + per, total);
   uint32_t s = 0;
-  for (uint32_t i = lo; i < hi; ++i) s += hist[i];
+  for (uint32_t i = lo; i < hi; ++i) s += BRP_LD(&hist[i]);
   part[threadIdx.x] = s;
   __syncthreads();
   for (int off = 1; off < 1024; off <<= 1) {
@@ -78,8 +78,8 @@ __global__ void __launch_bounds__(1024) rs_scan(uint32_t* hist, uint32_t total) 
   }
   uint32_t run = threadIdx.x ? part[threadIdx.x - 1] : 0u;
   for (uint32_t i = lo; i < hi; ++i) {
-    const uint32_t c = hist[i];
-    hist[i] = run;
+    const uint32_t c = BRP_LD(&hist[i]);
+    BRP_ST(&hist[i], run);
     run += c;
   }
 }
@@ -93,7 +93,7 @@ __global__ void __launch_bounds__(kRsThreads) rs_scatter(const uint32_t* kin, co
   constexpr int kWaves = kRsThreads / kWave;
   __shared__ uint32_t base[256];
   __shared__ uint32_t wcnt[kWaves][256];
-  base[threadIdx.x] = offs[threadIdx.x * nblocks + blockIdx.x];
+  base[threadIdx.x] = BRP_LD(&offs[threadIdx.x * nblocks + blockIdx.x]);
 #pragma unroll
   for (int w = 0; w < kWaves; ++w) wcnt[w][threadIdx.x] = 0;
   __syncthreads();
@@ -103,8 +103,8 @@ __global__ void __launch_bounds__(kRsThreads) rs_scatter(const uint32_t* kin, co
   for (int r = 0; r < kRsPer; ++r) {
     const uint32_t i = b0 + r * kRsThreads + threadIdx.x;
     const bool valid = i < n;
-    const uint32_t k = valid ? kin[i] : 0u;
-    const uint32_t v = valid ? vin[i] : 0u;
+    const uint32_t k = valid ? BRP_LD(&kin[i]) : 0u;
+    const uint32_t v = valid ? BRP_LD(&vin[i]) : 0u;
     const uint32_t d = (k >> shift) & 255u;
     unsigned long long same = __ballot(valid);
 #pragma unroll
@@ -120,8 +120,8 @@ __global__ void __launch_bounds__(kRsThreads) rs_scatter(const uint32_t* kin, co
       uint32_t pre = 0;
       for (int w = 0; w < wave; ++w) pre += wcnt[w][d];
       const uint32_t pos = base[d] + pre + rw;
-      kout[pos] = k;
-      vout[pos] = v;
+      BRP_ST(&kout[pos], k);
+      BRP_ST(&vout[pos], v);
     }
     __syncthreads();
     uint32_t add = 0;
@@ -137,7 +137,7 @@ __global__ void __launch_bounds__(kRsThreads) rs_scatter(const uint32_t* kin, co
 
 __global__ void __launch_bounds__(kRsThreads) rs_rank(const uint32_t* sp, uint32_t n, uint32_t* rank) {
   const uint32_t e = blockIdx.x * kRsThreads + threadIdx.x;
-  if (e < n) rank[sp[e]] = e;
+  if (e < n) BRP_ST(&rank[BRP_LD(&sp[e])], e);
 }
 
 // one wave per run of kRmedRun outputs
@@ -161,7 +161,7 @@ __global__ void __launch_bounds__(kWave) rmed_wide_kernel(const float* in, uint3
     for (int q = 0; q < 4; ++q) hist[lane + 64 * q] = 0;
     __syncthreads();
     for (uint32_t p = t0 + lane; p < t0 + W; p += kWave) {
-      const uint32_t r = rank[p];
+      const uint32_t r = BRP_LD(&rank[p]);
       if ((static_cast<uint64_t>(r) >> (shift + width)) == prefix) atomicAdd(&hist[(r >> shift) & ((1u << width) - 1u)], 1u);
     }
     __syncthreads();
@@ -201,7 +201,7 @@ __global__ void __launch_bounds__(kWave) rmed_wide_kernel(const float* in, uint3
   uint32_t below = mid;    // members with sorted index < m
 
   auto is_member = [&](uint32_t e, uint32_t t) -> bool {
-    const uint32_t p = sp[e];
+    const uint32_t p = BRP_LD(&sp[e]);
     return (p - t) < W;
   };
   // first member with sorted index >= e (exists: the window has W members)
@@ -213,7 +213,7 @@ __global__ void __launch_bounds__(kWave) rmed_wide_kernel(const float* in, uint3
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const uint32_t x = e + lane + kWave * q;
-        f[q] = x < n_in && ((sp[x] - t) < W);
+        f[q] = x < n_in && ((BRP_LD(&sp[x]) - t) < W);
       }
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -230,7 +230,7 @@ __global__ void __launch_bounds__(kWave) rmed_wide_kernel(const float* in, uint3
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const uint32_t off = static_cast<uint32_t>(lane + kWave * q);
-        f[q] = off <= e && ((sp[e - off] - t) < W);
+        f[q] = off <= e && ((BRP_LD(&sp[e - off]) - t) < W);
       }
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -247,18 +247,18 @@ __global__ void __launch_bounds__(kWave) rmed_wide_kernel(const float* in, uint3
     if (step % kWave == 0) {
       // ranks leaving / entering over the next 64 slides
       const uint32_t po = t + lane, pi = t + W + lane;
-      ro_v = po < n_in ? rank[po] : 0u;
-      ri_v = pi < n_in ? rank[pi] : 0u;
+      ro_v = po < n_in ? BRP_LD(&rank[po]) : 0u;
+      ri_v = pi < n_in ? BRP_LD(&rank[pi]) : 0u;
     }
-    const float a = in[sp[m]];
+    const float a = BRP_LD(&in[BRP_LD(&sp[m])]);
     float out;
     if (odd) {
       out = a;
     } else {
-      const float b = in[sp[next_member(m + 1, t)]];
+      const float b = BRP_LD(&in[BRP_LD(&sp[next_member(m + 1, t)])]);
       out = static_cast<float>(static_cast<double>(a + b) / 2.0);
     }
-    if (lane == 0) med[t] = out;
+    if (lane == 0) BRP_ST(&med[t], out);
     if (t + 1 >= t1) break;
     const uint32_t ro = __shfl(ro_v, static_cast<int>(step % kWave), kWave);
     const uint32_t ri = __shfl(ri_v, static_cast<int>(step % kWave), kWave);
@@ -302,19 +302,19 @@ hipError_t launch_running_median_wide(const float* in, uint32_t n_in, uint32_t W
   uint32_t* rank = base + 4ull * n_in;
   uint32_t* hist = base + 5ull * n_in;
   const dim3 eg((n_in + kRsThreads - 1) / kRsThreads);
-  hipLaunchKernelGGL(rs_init, eg, dim3(kRsThreads), 0, s, in, n_in, keys[0], vals[0]);
+  BRP_LAUNCH(rs_init, eg, dim3(kRsThreads), 0, s, in, n_in, keys[0], vals[0]);
   for (int pass = 0; pass < 4; ++pass) {
     const int src = pass & 1, dst = src ^ 1;
-    hipLaunchKernelGGL(rs_hist, dim3(nblocks), dim3(kRsThreads), 0, s, keys[src], n_in, 8 * pass, hist, nblocks);
-    hipLaunchKernelGGL(rs_scan, dim3(1), dim3(1024), 0, s, hist, 256u * nblocks);
-    hipLaunchKernelGGL(rs_scatter, dim3(nblocks), dim3(kRsThreads), 0, s, keys[src], vals[src], keys[dst], vals[dst],
+    BRP_LAUNCH(rs_hist, dim3(nblocks), dim3(kRsThreads), 0, s, keys[src], n_in, 8 * pass, hist, nblocks);
+    BRP_LAUNCH(rs_scan, dim3(1), dim3(1024), 0, s, hist, 256u * nblocks);
+    BRP_LAUNCH(rs_scatter, dim3(nblocks), dim3(kRsThreads), 0, s, keys[src], vals[src], keys[dst], vals[dst],
                        n_in, 8 * pass, hist, nblocks);
   }
   // four passes: the sorted positions are back in vals[0]
-  hipLaunchKernelGGL(rs_rank, eg, dim3(kRsThreads), 0, s, vals[0], n_in, rank);
+  BRP_LAUNCH(rs_rank, eg, dim3(kRsThreads), 0, s, vals[0], n_in, rank);
   const dim3 rg((n_out + kRmedRun - 1) / kRmedRun);
-  hipLaunchKernelGGL(rmed_wide_kernel, rg, dim3(kWave), 0, s, in, n_in, W, vals[0], rank, med, n_out, bits_for(n_in));
-  return hipGetLastError();
+  BRP_LAUNCH(rmed_wide_kernel, rg, dim3(kWave), 0, s, in, n_in, W, vals[0], rank, med, n_out, bits_for(n_in));
+  return launch_status();
 }
 
 }  // namespace hipk

@@ -16,10 +16,11 @@ __global__ void whiten_power_kernel(const float2* spec, uint32_t n, float* ps) {
   if (k >= n) return;
   float p = 0.0f;
   if (k != 0) {
-    const double re = spec[k].x, im = spec[k].y;
+    const float2 sk = BRP_LD(&spec[k]);
+    const double re = sk.x, im = sk.y;
     p = static_cast<float>(re * re + im * im);
   }
-  ps[k] = p;
+  BRP_ST(&ps[k], p);
 }
 
 // Exact running median. Each workgroup sorts (value, position) of its span of
@@ -58,7 +59,7 @@ __device__ __forceinline__ void rmed_sort_reg(const float* in, uint32_t n_in, ui
   for (int j = 0; j < 16; ++j) {
     const int e = 16 * t + j;
     const uint32_t g = o0 + e;
-    const float k = (e < static_cast<int>(per_block + W - 1) && g < n_in) ? in[g] : __builtin_inff();
+    const float k = (e < static_cast<int>(per_block + W - 1) && g < n_in) ? BRP_LD(&in[g]) : __builtin_inff();
     v[j] = (static_cast<uint64_t>(ord_bits(k)) << 16) | static_cast<uint32_t>(e);
   }
   uint32_t* keyu = reinterpret_cast<uint32_t*>(key);
@@ -134,7 +135,7 @@ __global__ void __launch_bounds__(NT) running_median_kernel(const float* in, uin
   } else {
   for (int t = threadIdx.x; t < SPAN; t += NT) {
     const uint32_t g = o0 + t;
-    key[t] = (t < static_cast<int>(per_block + W - 1) && g < n_in) ? in[g] : __builtin_inff();
+    key[t] = (t < static_cast<int>(per_block + W - 1) && g < n_in) ? BRP_LD(&in[g]) : __builtin_inff();
     pos[t] = static_cast<uint16_t>(t);
   }
   __syncthreads();
@@ -245,7 +246,7 @@ __global__ void __launch_bounds__(NT) running_median_kernel(const float* in, uin
       b = key[next_member(m + 1, t)];
     }
     const float a = key[m];
-    med[o0 + t] = odd ? a : static_cast<float>(static_cast<double>(a + b) / 2.0);
+    BRP_ST(&med[o0 + t], odd ? a : static_cast<float>(static_cast<double>(a + b) / 2.0));
     if (t + 1 >= t1) break;
     // slide: remove position t, insert position t + W
     const int ro = rank[t], ri = rank[t + W];
@@ -272,32 +273,32 @@ __global__ void unpack_kernel(const uint8_t* packed, uint32_t n_packed, bool fou
   if (four_bit) {
     const uint32_t b = i >> 1;
     if (b < n_packed) {
-      const uint8_t c = packed[b];
+      const uint8_t c = BRP_LD(&packed[b]);
       const uint32_t nib = (i & 1u) ? (c & 15u) : (c >> 4);
       v = static_cast<float>(static_cast<double>(static_cast<float>(nib)) / scale);
     }
   } else if (i < n_packed) {
-    v = static_cast<float>(static_cast<double>(static_cast<int8_t>(packed[i])) / scale);
+    v = static_cast<float>(static_cast<double>(static_cast<int8_t>(BRP_LD(&packed[i]))) / scale);
   }
-  out[i] = v;
+  BRP_ST(&out[i], v);
 }
 
 // spec[w2 + i] *= sqrt(ln2 / med[i]) for i < white_size
 __global__ void whiten_scale_kernel(float2* spec, const float* med, uint32_t white_size, uint32_t w2) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= white_size) return;
-  const float f = static_cast<float>(sqrt(M_LN2 / static_cast<double>(med[i])));
-  float2 v = spec[i + w2];
+  const float f = static_cast<float>(sqrt(M_LN2 / static_cast<double>(BRP_LD(&med[i]))));
+  float2 v = BRP_LD(&spec[i + w2]);
   v.x *= f;
   v.y *= f;
-  spec[i + w2] = v;
+  BRP_ST(&spec[i + w2], v);
 }
 
 __global__ void zap_kernel(float2* spec, uint32_t fft_size, const uint32_t* bins, const float2* noise, uint32_t n) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const uint32_t k = bins[i];
-  if (k < fft_size) spec[k] = noise[i];
+  const uint32_t k = BRP_LD(&bins[i]);
+  if (k < fft_size) BRP_ST(&spec[k], BRP_LD(&noise[i]));
 }
 
 // Inverse real-FFT packing: Z_k = (X_k + conj X_{M-k}) + i W_N^{-k} (X_k - conj X_{M-k}),
@@ -308,7 +309,7 @@ __global__ void tangle_kernel(const float2* spec, uint32_t M, uint32_t fft_size,
   if (k >= M) return;
   auto bin = [&](uint32_t q) -> float2 {
     if (q < w2 || q >= fft_size - w2) return make_float2(0.0f, 0.0f);
-    float2 v = spec[q];
+    float2 v = BRP_LD(&spec[q]);
     if (q == 0 || q == M) v.y = 0.0f;
     return v;
   };
@@ -317,7 +318,7 @@ __global__ void tangle_kernel(const float2* spec, uint32_t M, uint32_t fft_size,
   const float2 w = conjf2(tw_lookup32(tw, 2u * k));  // W_N^{-k}
   const float2 d = csub(a, bc);
   const float2 iwd = cmul(make_float2(0.0f, 1.0f), cmul(w, d));
-  z[k] = cadd(cadd(a, bc), iwd);
+  BRP_ST(&z[k], cadd(cadd(a, bc), iwd));
 }
 
 }  // namespace
@@ -325,14 +326,14 @@ __global__ void tangle_kernel(const float2* spec, uint32_t M, uint32_t fft_size,
 hipError_t launch_unpack(const uint8_t* packed, uint32_t n_packed, bool four_bit, double scale, float* out,
                          uint32_t n_out, hipStream_t s) {
   if (n_out == 0) return hipSuccess;
-  hipLaunchKernelGGL(unpack_kernel, dim3((n_out + 255) / 256), dim3(256), 0, s, packed, n_packed, four_bit, scale, out,
+  BRP_LAUNCH(unpack_kernel, dim3((n_out + 255) / 256), dim3(256), 0, s, packed, n_packed, four_bit, scale, out,
                      n_out);
-  return hipGetLastError();
+  return launch_status();
 }
 
 hipError_t launch_whiten_power(const float2* spec, uint32_t n, float* ps, hipStream_t s) {
-  hipLaunchKernelGGL(whiten_power_kernel, dim3((n + 255) / 256), dim3(256), 0, s, spec, n, ps);
-  return hipGetLastError();
+  BRP_LAUNCH(whiten_power_kernel, dim3((n + 255) / 256), dim3(256), 0, s, spec, n, ps);
+  return launch_status();
 }
 
 // LDS spans: 4096 entries (32 KB) up to W = 3072, 16384 entries (128 KB, one
@@ -353,9 +354,9 @@ hipError_t launch_running_median(const float* in, uint32_t n_in, uint32_t W, flo
       return hipErrorInvalidConfiguration;
     constexpr int kSpanL = 16384, kThreadsL = 1024;
     const uint32_t perL = kSpanL - W + 1;
-    hipLaunchKernelGGL((running_median_kernel<kSpanL, kThreadsL, true>), dim3((n_out + perL - 1) / perL),
+    BRP_LAUNCH((running_median_kernel<kSpanL, kThreadsL, true>), dim3((n_out + perL - 1) / perL),
                        dim3(kThreadsL), 0, s, in, n_in, W, med, n_out, perL);
-    return hipGetLastError();
+    return launch_status();
   }
   constexpr int kSpan = 4096, kThreads = 256;
   const uint32_t per = kSpan - W + 1;
@@ -366,33 +367,33 @@ hipError_t launch_running_median(const float* in, uint32_t n_in, uint32_t W, flo
   // MI355X, bit-exact; profiles/README.md round 3); BRP_RMED_REG=0: LDS bitonic
   static const bool reg = std::getenv("BRP_RMED_REG") == nullptr || std::atoi(std::getenv("BRP_RMED_REG")) != 0;
   if (reg && !plain)
-    hipLaunchKernelGGL((running_median_kernel<kSpan, kThreads, true, true>), dim3((n_out + per - 1) / per),
+    BRP_LAUNCH((running_median_kernel<kSpan, kThreads, true, true>), dim3((n_out + per - 1) / per),
                        dim3(kThreads), 0, s, in, n_in, W, med, n_out, per, walkers);
   else if (plain)
-    hipLaunchKernelGGL((running_median_kernel<kSpan, kThreads, false>), dim3((n_out + per - 1) / per), dim3(kThreads), 0,
+    BRP_LAUNCH((running_median_kernel<kSpan, kThreads, false>), dim3((n_out + per - 1) / per), dim3(kThreads), 0,
                        s, in, n_in, W, med, n_out, per);
   else
-    hipLaunchKernelGGL((running_median_kernel<kSpan, kThreads, true>), dim3((n_out + per - 1) / per), dim3(kThreads), 0,
+    BRP_LAUNCH((running_median_kernel<kSpan, kThreads, true>), dim3((n_out + per - 1) / per), dim3(kThreads), 0,
                        s, in, n_in, W, med, n_out, per);
-  return hipGetLastError();
+  return launch_status();
 }
 
 hipError_t launch_whiten_scale(float2* spec, const float* med, uint32_t white_size, uint32_t w2, hipStream_t s) {
-  hipLaunchKernelGGL(whiten_scale_kernel, dim3((white_size + 255) / 256), dim3(256), 0, s, spec, med, white_size, w2);
-  return hipGetLastError();
+  BRP_LAUNCH(whiten_scale_kernel, dim3((white_size + 255) / 256), dim3(256), 0, s, spec, med, white_size, w2);
+  return launch_status();
 }
 
 hipError_t launch_zap(float2* spec, uint32_t fft_size, const uint32_t* bins, const float2* noise, uint32_t n,
                       hipStream_t s) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(zap_kernel, dim3((n + 255) / 256), dim3(256), 0, s, spec, fft_size, bins, noise, n);
-  return hipGetLastError();
+  BRP_LAUNCH(zap_kernel, dim3((n + 255) / 256), dim3(256), 0, s, spec, fft_size, bins, noise, n);
+  return launch_status();
 }
 
 hipError_t launch_tangle(const float2* spec, uint32_t M, uint32_t fft_size, uint32_t w2, const TwiddleTable& tw,
                          float2* z, hipStream_t s) {
-  hipLaunchKernelGGL(tangle_kernel, dim3((M + 255) / 256), dim3(256), 0, s, spec, M, fft_size, w2, tw, z);
-  return hipGetLastError();
+  BRP_LAUNCH(tangle_kernel, dim3((M + 255) / 256), dim3(256), 0, s, spec, M, fft_size, w2, tw, z);
+  return launch_status();
 }
 
 }  // namespace hipk

@@ -44,3 +44,19 @@ def gpu(has_gpu):
 @pytest.fixture()
 def tmpdir_path(tmp_path):
     return tmp_path
+
+
+@pytest.fixture(autouse=True)
+def _device_fault_check(request):
+    """After every GPU test: synchronise the device and fail THIS test if any
+    of its work faulted (brp.device_check: hipDeviceSynchronize +
+    hipGetLastError; in the checked build also the kernel, source line and
+    address of an out-of-bounds access or guard-zone write). A device fault is
+    then charged to the test that caused it, not to whichever later call
+    happens to notice it (round-5 verdict)."""
+    yield
+    if request.node.get_closest_marker("gpu") is None:
+        return
+    import boinc_app_eah_brp_amd as pkg
+
+    pkg.native().device_check()
