@@ -485,6 +485,11 @@ struct HipEngine::Impl {
   bool hs_xcd = false;          // pruned HS: contiguous block ranges per XCD (BRP_HS_XCD=1)
   bool lds_pass1 = false;       // resampling pass 1 on the LDS-staged kernel (BRP_P1_LDS=1, A/B)
   bool mid_waves = false;       // pass3_mid: whole-wave workgroups of 16 / 32 rows (BRP_MID_WAVES=1, A/B)
+  // 8-bin bound cells of the own bins written by pass 3 (pass3_kernel CELLS),
+  // hs_cells_kernel only for the mirror half; BRP_P3_CELLS=1 (A/B, default off:
+  // profiles/README.md round 6)
+  bool p3_cells = false;
+  bool fused_cells() const { return p3_cells && hs_prune && hs_cell_shift == 3 && !bs; }
   bool hs_direct = true;        // bounds read straight from global memory (BRP_HS_DIRECT=0: LDS-staged;
                                 // +2 % fp32, +3 % config 5 in one call, profiles/README.md round 3)
   DevBuf<double> partials;      // [batch][wg1]
@@ -876,8 +881,11 @@ struct HipEngine::Impl {
     a2.delta = delta.p;
     return hipk::launch_pass2(plan, a2, nb, stream);
   }
-  // row pass + untangle + power spectrum into out[b * stride + k], k < limit
-  hipError_t fft_pass3(int nb, float* out, _Float16* out16, uint32_t stride, uint32_t limit) {
+  // row pass + untangle + power spectrum into out[b * stride + k], k < limit;
+  // with_cells: also the pruned harmonic sum's 8-bin bound cells of the own
+  // (low-residue) bins (pyr), so that the harmonic sum re-reads only half the
+  // spectrum for the others
+  hipError_t fft_pass3(int nb, float* out, _Float16* out16, uint32_t stride, uint32_t limit, bool with_cells = false) {
     hipk::Pass3Args a3{};
     a3.buf = buf.p;
     a3.L1 = plan.L1;
@@ -894,6 +902,11 @@ struct HipEngine::Impl {
     a3.norm = static_cast<float>(1.0 / g.nsamples);
     a3.tmpl = tmpl.p;
     a3.delta = delta.p;
+    if (with_cells) {
+      a3.cells = pyr.p;
+      a3.cells_stride = hipk::hs_pyr_stride(ps_stride);
+      a3.n_cells = (ps_stride >> 3) + 8;  // what hs_cells_kernel writes (8-bin cells)
+    }
     return hipk::launch_pass3(plan, hipk::P3_POWER, a3, nb, stream);
   }
 
@@ -922,7 +935,7 @@ struct HipEngine::Impl {
                                    std::min(g.harmonic_idx_hi, g.fft_size));
         }
         return fft_pass3(nb, ps.p, ps_fp16 ? reinterpret_cast<_Float16*>(ps.p) : nullptr, ps_stride,
-                         std::min(g.harmonic_idx_hi, g.fft_size));
+                         std::min(g.harmonic_idx_hi, g.fft_size), fused_cells());
       }
       case kHarmonic: {
         hipk::HSArgs ah{};
@@ -943,6 +956,9 @@ struct HipEngine::Impl {
         ah.xcd = hs_xcd;
         ah.pyr = pyr.p;
         ah.pyr_stride = hipk::hs_pyr_stride(ps_stride);
+        ah.cells_ready = !bs && fused_cells();  // pass 3 wrote the own-bin cells
+        ah.row_c = plan.L1 * plan.L2;
+        ah.row_l = plan.L3;
         ah.key_base = key_base;
         ah.bin_bits = bin_bits;
         if (select_mode) {
@@ -1298,6 +1314,7 @@ int HipEngine::setup_impl(const SearchGeometry& g, const float* host_series, con
   if (const char* e = std::getenv("BRP_FG_INPLACE_MAX"))
     d.inplace_max = std::min<uint32_t>(d.kcopy, static_cast<uint32_t>(std::max(0, std::atoi(e))));
   d.hs_direct = std::getenv("BRP_HS_DIRECT") == nullptr || std::atoi(std::getenv("BRP_HS_DIRECT")) != 0;
+  d.p3_cells = std::getenv("BRP_P3_CELLS") != nullptr && std::atoi(std::getenv("BRP_P3_CELLS")) != 0;
   d.hs_xcd = std::getenv("BRP_HS_XCD") != nullptr && std::atoi(std::getenv("BRP_HS_XCD")) == 1;
   d.lds_pass1 = std::getenv("BRP_P1_LDS") != nullptr && std::atoi(std::getenv("BRP_P1_LDS")) == 1;
   d.mid_waves = std::getenv("BRP_MID_WAVES") != nullptr && std::atoi(std::getenv("BRP_MID_WAVES")) == 1;
@@ -1870,7 +1887,12 @@ int HipEngine::complete(std::vector<TemplateCands>& out) {
   for (uint32_t q = 0; q < cnt; ++q) {
     const uint32_t key = src[q].x;
     const uint32_t k = static_cast<uint32_t>(static_cast<uint64_t>(key) >> (bb + 3)), h = (key >> bb) & 7u;
-    if (k >= static_cast<uint32_t>(nb) || h >= static_cast<uint32_t>(kNumHarmonicLevels)) return RADPUL_EVAL;
+    if (k >= static_cast<uint32_t>(nb) || h >= static_cast<uint32_t>(kNumHarmonicLevels)) {
+      log_message(LOG_ERROR, true,
+                  "Candidate %u of %u has key 0x%08x (template %u of %d, level %u; bounded output %d, list %s).\n", q,
+                  cnt, key, k, nb, h, ran_select ? 1 : 0, extra ? "copied" : "in place");
+      return RADPUL_EVAL;
+    }
     float p;
     std::memcpy(&p, &src[q].y, sizeof(float));
     out[k].level[h].push_back(BinPower{key & bin_mask, p});

@@ -119,7 +119,10 @@ __device__ ChkDev* g_chk_dev = nullptr;
 hipError_t chk_bind_this_tu(ChkDev* p) { return hipMemcpyToSymbol(HIP_SYMBOL(g_chk_dev), &p, sizeof(p)); }
 [[maybe_unused]] const int g_chk_tu_registered = chk_register_binder(&chk_bind_this_tu);
 
-__device__ __noinline__ void chk_record(ChkDev* c, uint64_t a, uint32_t bytes, uint32_t line, bool st) {
+// inlined, as chk_addr: an out-of-line call in divergent code before a
+// wave-aggregated emit (ballot, leader atomic, broadcast) left holes in the
+// candidate list of the select path (round 6, the first checked build)
+__device__ __forceinline__ void chk_record(ChkDev* c, uint64_t a, uint32_t bytes, uint32_t line, bool st) {
   if (atomicCAS(&c->fault, 0u, 1u) != 0u) return;
   c->line = line;
   c->addr = a;
@@ -132,7 +135,7 @@ __device__ __noinline__ void chk_record(ChkDev* c, uint64_t a, uint32_t bytes, u
 }
 
 // [p, p + bytes) inside one live allocation (binary search of the sorted ranges)
-__device__ __noinline__ bool chk_addr(const void* p, uint32_t bytes, uint32_t line, bool st) {
+__device__ __forceinline__ bool chk_addr(const void* p, uint32_t bytes, uint32_t line, bool st) {
   ChkDev* c = g_chk_dev;
   if (c == nullptr) return true;
   const uint64_t a = reinterpret_cast<uint64_t>(p);

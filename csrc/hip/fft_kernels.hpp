@@ -125,6 +125,11 @@ struct Pass3Args {
   const double* delta;         // [batch] mean-padding correction (pass 2)
   // P3_COMPLEX
   float2* spec;                // fft_size complex bins
+  // P3_POWER with the pruned harmonic sum's 8-bin bound cells fused (when
+  // non-null): cells[b * cells_stride + j] = max of bins 8j .. 8j + 7 (0 past
+  // limit); the caller zeroes them first
+  float* cells;
+  uint32_t cells_stride, n_cells;
 };
 
 // Middle of a chirp-z convolution (bluestein_kernels.hpp), in place on the

@@ -1107,8 +1107,18 @@ struct P3Emit {
   }
 };
 
-template <int L, int ROWS, int MODE>
+// CELLS (power modes, a.cells set): the pruned harmonic sum's 8-bin bound
+// cells of the rows' own bins fused into the untangle: the 8 rows c0 .. c0 + 7
+// of a workgroup are the 8 consecutive bins of one aligned cell for every k3,
+// held by 8 consecutive lanes (three shuffles), and no other workgroup writes
+// that cell (residues below C/2). Their mirror bins M - k fall into two cells
+// shared with the neighbouring workgroup: those cells (residues >= C/2) are
+// left to hs_cells_kernel's mirror-half mode, which then reads half the
+// spectrum. (A first form wrote the mirror cells too, with device-scope
+// atomic max: pass 3 went from 41.9 to 74.0 us per template, round 6.)
+template <int L, int ROWS, int MODE, bool CELLS = false>
 __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Args a) {
+  static_assert(!CELLS || ROWS == 8, "fused cells: one workgroup row group per 8-bin cell");
   constexpr int TPC = tpc_for<L>();
   constexpr int NSLOT = 2 * ROWS;
   constexpr int NT = NSLOT * TPC;
@@ -1235,7 +1245,17 @@ __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Arg
   // rotations: W_2N^k and W_2N^{n_s k} are stepped by one complex multiply per
   // bin (a few ulp over L / kStreams steps) instead of two table products.
   static_assert(L % kStreams == 0, "whole untangle iterations");
-  if (c <= half) {
+  const bool live = c <= half;  // rows beyond C/2 are the mirrors of others
+  // cells of this template; the workgroup's own cells are its alone unless its
+  // rows reach C/2 (that cell also holds mirror bins of the workgroup before)
+  float* const cells = CELLS ? a.cells + static_cast<size_t>(b) * a.cells_stride : nullptr;
+  const bool own_excl = c0 + ROWS <= half;  // the workgroup at C/2 leaves its cell to hs_cells_kernel
+  auto group_max = [](float v) {
+    v = fmaxf(v, __shfl_xor(v, 1, 8));
+    v = fmaxf(v, __shfl_xor(v, 2, 8));
+    return fmaxf(v, __shfl_xor(v, 4, 8));
+  };
+  if (CELLS || live) {
     float2 tk = cmul(rt.t1, w4(static_cast<uint32_t>(t)));  // W_2N^k for k3 = t
     const float2 tk_step = w4(static_cast<uint32_t>(kStreams));
     float2 ta = make_float2(0.f, 0.f), ta_step = make_float2(1.f, 0.f);
@@ -1257,14 +1277,25 @@ __global__ void __launch_bounds__(2 * ROWS * tpc_for<L>()) pass3_kernel(Pass3Arg
       const float2 zm = data[Lay::idx(k3m, c == 0 ? s : ROWS + s)];
       const uint32_t k = c + a.C * static_cast<uint32_t>(k3);
       const float2 w = cmul(tk, tk);          // W_N^k
-      emit(k, untangle_w(zk, zm, w), tk, ta);
-      if (c != 0 && c != half) {
-        const uint32_t kk = a.M - k;                 // = cm + C*(L-1-k3)
-        const float2 tkm = make_float2(-tk.y, -tk.x);  // W_2N^{M-k} = -i conj(W_2N^k)
-        const float2 tam = cmulc(rq, ta);
-        emit(kk, untangle_wm(zm, zk, w), tkm, tam);
+      float v_own = 0.0f, v_mir = 0.0f, v_nyq = 0.0f;
+      if (live) {
+        v_own = emit(k, untangle_w(zk, zm, w), tk, ta);
+        if (c != 0 && c != half) {
+          const uint32_t kk = a.M - k;                 // = cm + C*(L-1-k3)
+          const float2 tkm = make_float2(-tk.y, -tk.x);  // W_2N^{M-k} = -i conj(W_2N^k)
+          const float2 tam = cmulc(rq, ta);
+          v_mir = emit(kk, untangle_wm(zm, zk, w), tkm, tam);
+        }
+        if (c == 0 && k3 == 0) v_nyq = emit.nyquist(zk, n_s);
       }
-      if (c == 0 && k3 == 0) emit.nyquist(zk, n_s);
+      if constexpr (CELLS) {
+        // every own cell is written, zeros included (bins past the limit):
+        // the buffer is not cleared between batches
+        const float m_own = group_max(v_own);
+        const uint32_t idx = (c0 >> 3) + (a.C >> 3) * static_cast<uint32_t>(k3);
+        if (s == 0 && own_excl && idx < a.n_cells) BRP_ST(&cells[idx], m_own);
+      }
+      (void)v_nyq;
     }
   }
 }
@@ -1578,8 +1609,12 @@ hipError_t launch_pass3(const FFTPlan3& plan, Pass3Mode mode, const Pass3Args& a
 #define X(n)                                                                                              \
   case n: {                                                                                               \
     const dim3 block(2 * kRowsP * tpc_for<n>());                                                          \
-    if (mode == P3_POWER && a.ps16)                                                                       \
-      BRP_LAUNCH((pass3_kernel<n, kRowsP, P3_POWER16>), grid, block, 0, s, a);                    \
+    if (mode == P3_POWER && a.ps16 && a.cells)                                                            \
+      BRP_LAUNCH((pass3_kernel<n, kRowsP, P3_POWER16, true>), grid, block, 0, s, a);                      \
+    else if (mode == P3_POWER && a.ps16)                                                                  \
+      BRP_LAUNCH((pass3_kernel<n, kRowsP, P3_POWER16>), grid, block, 0, s, a);                            \
+    else if (mode == P3_POWER && a.cells)                                                                 \
+      BRP_LAUNCH((pass3_kernel<n, kRowsP, P3_POWER, true>), grid, block, 0, s, a);                        \
     else if (mode == P3_POWER) BRP_LAUNCH((pass3_kernel<n, kRowsP, P3_POWER>), grid, block, 0, s, a); \
     else BRP_LAUNCH((pass3_kernel<n, kRowsP, P3_COMPLEX>), grid, block, 0, s, a);                 \
     break;                                                                                                \

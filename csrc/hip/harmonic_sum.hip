@@ -213,12 +213,19 @@ __device__ __forceinline__ const PsT<MODE>* ps_row(const HSArgs& a, int b) {
   else return a.ps16 + static_cast<size_t>(b) * a.ps_stride;
 }
 
-// maxima of the spectrum over cells of 2^CK bins (fp32 cells for either spectrum)
-template <int CK, int MODE>
+// maxima of the spectrum over cells of 2^CK bins (fp32 cells for either
+// spectrum). REST (a.cells_ready, 8-bin cells): only the cells pass 3 did not
+// write -- residues >= C/2 of the rows k3 < L3 (thread u -> row u / (C/16)),
+// then every cell from M/8 on
+template <int CK, int MODE, bool REST = false>
 __global__ void __launch_bounds__(256) hs_cells_kernel(HSArgs a) {
   constexpr int W = 1 << CK;
   const int b = blockIdx.y;
-  const uint32_t m = blockIdx.x * 256u + threadIdx.x;
+  uint32_t m = blockIdx.x * 256u + threadIdx.x;
+  if constexpr (REST) {
+    const uint32_t per = a.row_c >> 4, nm = per * a.row_l;
+    m = m < nm ? (m / per) * (a.row_c >> 3) + per + m % per : (a.row_c >> 3) * a.row_l + (m - nm);
+  }
   if (m >= (a.ps_stride >> CK) + 8) return;
   const PsT<MODE>* P = ps_row<MODE>(a, b);
   const uint32_t k0 = W * m;
@@ -848,10 +855,15 @@ hipError_t launch_harmonic_sum(const HSArgs& a, int batch, hipStream_t s) {
     const uint32_t nblk = hs_num_blocks(a.i_start, a.hhi);
     if (nblk == 0) return hipSuccess;
     const dim3 gc((hs_pyr_stride(a.ps_stride) + 255) / 256, batch), gp((nblk + 255) / 256, batch);
-#define BRP_HS_PRUNED(CK, MODE, DIRECT)                                              \
-  do {                                                                              \
-    BRP_LAUNCH((hs_cells_kernel<CK, MODE>), gc, dim3(256), 0, s, a);         \
-    BRP_LAUNCH((hs_pruned_kernel<CK, MODE, DIRECT>), gp, dim3(256), 0, s, a, nblk); \
+    // cells pass 3 left (cells_ready): the mirror half of rows k3 < L3, then the cells from M/8 on
+    const uint32_t n8 = (a.ps_stride >> 3) + 8, m8 = (a.row_c >> 3) * a.row_l;
+    const uint32_t n_rest = (a.row_c >> 4) * a.row_l + (n8 > m8 ? n8 - m8 : 0u);
+    const dim3 gr((n_rest + 255) / 256, batch);
+#define BRP_HS_PRUNED(CK, MODE, DIRECT)                                                    \
+  do {                                                                                    \
+    if (CK == 3 && a.cells_ready) BRP_LAUNCH((hs_cells_kernel<CK, MODE, true>), gr, dim3(256), 0, s, a); \
+    else BRP_LAUNCH((hs_cells_kernel<CK, MODE>), gc, dim3(256), 0, s, a);                \
+    BRP_LAUNCH((hs_pruned_kernel<CK, MODE, DIRECT>), gp, dim3(256), 0, s, a, nblk);       \
   } while (0)
     if (a.mode == HS_F16) {
       if (a.cell_shift == 2) BRP_HS_PRUNED(2, HS_F16, false);

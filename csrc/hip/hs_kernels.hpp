@@ -37,6 +37,11 @@ struct HSArgs {
   bool xcd;     // pruned kernel: contiguous block ranges per XCD (BRP_HS_XCD=1, experiment)
   float* pyr;
   uint32_t pyr_stride;
+  // 8-bin cells of the bins with residue mod row_c below row_c / 2 already
+  // written (pass 3 fused them, rows of row_c bins, row_l rows up to M): the
+  // cell kernel computes only the others (mirror half and past M)
+  bool cells_ready;
+  uint32_t row_c, row_l;
   uint32_t key_base;  // index of template 0 of this launch within the batch's candidate list
   uint32_t bin_bits;  // candidate key layout (hs_pack): bins < 2^bin_bits
   float* dense;       // select path: [batch][5][dense_stride] level values (HsSelectArgs)

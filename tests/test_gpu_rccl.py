@@ -130,19 +130,22 @@ def _bench_json(args, env_extra, tmp):
     return json.loads(lines[0])
 
 
-def test_bench_self_launched_ranks_on_one_gpu(gpu, tmp_path):
-    """`bench.py --gpus 2` through its own launcher (launch_ranks: two Popen'd
+@pytest.mark.parametrize("nranks", [2, 4])
+def test_bench_self_launched_ranks_on_one_gpu(gpu, tmp_path, nranks):
+    """`bench.py --gpus N` through its own launcher (launch_ranks: N Popen'd
     rank processes, the floor exchange during the step, the all-gather and the
-    merge) with BRP_BENCH_SHARE_DEVICE=1, so that both ranks run on this box's
-    one GPU over gloo: the table equals the one-rank run's byte for byte. No
-    throughput is taken from it (the JSON line says so)."""
+    merge) with BRP_BENCH_SHARE_DEVICE=1, so that all ranks run on this box's
+    one GPU over gloo: the table equals the one-rank run's byte for byte. With
+    4 ranks FloorSync's all-reduce has more than two members (the 8-GPU node's
+    first run is otherwise its first execution at that size). No throughput is
+    taken from it (the JSON line says so)."""
     common = ["--templates", "200", "--steps", "1", "--warmup", "1"]
     one = _bench_json(["--gpus", "1", *common, "--write-output", str(tmp_path / "one.cand")], {}, tmp_path)
-    two = _bench_json(["--gpus", "2", *common, "--write-output", str(tmp_path / "two.cand")],
-                      {"BRP_BENCH_SHARE_DEVICE": "1"}, tmp_path)
-    assert two["n_gpus"] == 2 and two["launched_by"] == "bench.py", two
-    assert "shared_device" in two and "shared_device" not in one
-    assert two["floor_sync_rounds_last_step"] > 0, two
-    assert two["table_sha256"] == one["table_sha256"]
-    assert two["table_identical_to_warmup"] is True
-    assert (tmp_path / "one.cand").read_text() == (tmp_path / "two.cand").read_text()
+    many = _bench_json(["--gpus", str(nranks), *common, "--write-output", str(tmp_path / "many.cand")],
+                       {"BRP_BENCH_SHARE_DEVICE": "1"}, tmp_path)
+    assert many["n_gpus"] == nranks and many["launched_by"] == "bench.py", many
+    assert "shared_device" in many and "shared_device" not in one
+    assert many["floor_sync_rounds_last_step"] > 0, many
+    assert many["table_sha256"] == one["table_sha256"]
+    assert many["table_identical_to_warmup"] is True
+    assert (tmp_path / "one.cand").read_text() == (tmp_path / "many.cand").read_text()
