@@ -298,6 +298,19 @@ int SearchSession::open(const SearchOptions& opt, const SearchControl& ctl) {
   const int per_dev = d.opt.use_cpu ? 1 : std::max(1, ctl.pipelines);
   const int nback = ngpu * per_dev;
   boinc::begin_critical_section();
+  // each device's first pipeline warms up (code objects, the runtime's copy
+  // kernels) on a thread while the device's other pipelines create their
+  // streams: ~25 ms of one-time cost off the critical path (round 6,
+  // profiles/app_phases_r6.txt); BRP_WARM_UP=0: in line with the first work
+  static const bool warm = std::getenv("BRP_WARM_UP") == nullptr || std::atoi(std::getenv("BRP_WARM_UP")) != 0;
+  std::vector<std::thread> warmers;
+  struct WarmJoiner {
+    std::vector<std::thread>& w;
+    ~WarmJoiner() {
+      for (auto& t : w)
+        if (t.joinable()) t.join();
+    }
+  } join_warmers{warmers};
   for (int kb = 0; kb < nback; ++kb) {
     const int k = kb / per_dev;  // device index
     std::unique_ptr<Backend> b;
@@ -316,7 +329,14 @@ int SearchSession::open(const SearchOptions& opt, const SearchControl& ctl) {
       }
     }
     d.backends.push_back(std::move(b));
+    if (warm && !d.opt.use_cpu && kb % per_dev == 0 && per_dev > 1) {
+      Backend* first = d.backends.back().get();
+      warmers.emplace_back([first] {
+        if (const int rc = first->warm_up()) log_message(LOG_DEBUG, true, "Backend warm-up failed (%d).\n", rc);
+      });
+    }
   }
+  for (auto& t : warmers) t.join();
   boinc::end_critical_section();
   trace::phase("backends created");
   return 0;

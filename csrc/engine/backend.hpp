@@ -85,6 +85,9 @@ class Backend {
   }
   virtual int preferred_batch() const = 0;
   virtual int device() const { return -1; }
+  // one-time start-up costs of the backend's first work, callable on another
+  // thread before setup (HIP: code objects, copy kernels); 0 on success
+  virtual int warm_up() { return 0; }
   virtual BackendStats stats() const { return {}; }
   // Pipelined form of process(): up to max_in_flight() batches submitted
   // before the oldest is completed; complete() returns results in submission

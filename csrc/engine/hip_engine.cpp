@@ -264,7 +264,7 @@ hipError_t copy_sync(void* dst, const void* src, size_t bytes, hipMemcpyKind kin
 // a large-BAR device (all MI355X platforms) ROCm maps device memory into the
 // host address space at the same address. Checked with a host-written pattern
 // read back through a device copy.
-void* host_view(int device, void* p, size_t bytes, hipStream_t s) {
+void* host_view(int device, void* p, size_t bytes, hipStream_t s, PinnedBuf<uint8_t>& scratch) {
   int large_bar = 0;
   if (hipDeviceGetAttribute(&large_bar, hipDeviceAttributeIsLargeBar, device) != hipSuccess) return nullptr;
   hipPointerAttribute_t at{};
@@ -277,9 +277,9 @@ void* host_view(int device, void* p, size_t bytes, hipStream_t s) {
   for (size_t i = 0; i < bytes; ++i) pat[i] = static_cast<uint8_t>(i * 37u + 11u);
   std::memcpy(h, pat.data(), bytes);
   std::atomic_thread_fence(std::memory_order_seq_cst);
-  PinnedBuf<uint8_t> back;
-  if (back.alloc(bytes) || copy_sync(back.p, p, bytes, hipMemcpyDeviceToHost, s) != hipSuccess) return nullptr;
-  return std::memcmp(pat.data(), back.p, bytes) == 0 ? h : nullptr;
+  // read back through the engine's pinned stage (one allocation for all checks)
+  if (scratch.reserve(bytes) || copy_sync(scratch.p, p, bytes, hipMemcpyDeviceToHost, s) != hipSuccess) return nullptr;
+  return std::memcmp(pat.data(), scratch.p, bytes) == 0 ? h : nullptr;
 }
 
 // W_{2N}^j = exp(-i pi j / N) as a two-level float table
@@ -1169,6 +1169,33 @@ bool same_geometry(const SearchGeometry& a, const SearchGeometry& b) {
 }
 }  // namespace
 
+// One-time costs of the process's first work, paid here so that a caller can
+// overlap them with other start-up (search.cpp: pipeline 0's warm-up runs
+// while the other pipelines' streams are created): the device modules' code
+// objects (loaded at the first launch otherwise, ~14 ms), the runtime's copy
+// kernels (first copy on a stream, ~11 ms), the pinned stage.
+int HipEngine::warm_up() {
+  Impl& d = *impl_;
+  trace::Range range("brp:warm_up");
+  BRP_HIP_CHECK(hipSetDevice(d.device), RADPUL_HIP_DEVICE_SET);
+  for (hipError_t (*f)() : {hipk::preload_fft_passes, hipk::preload_harmonic_sum, hipk::preload_whiten,
+                            hipk::preload_resample, hipk::preload_bluestein, hipk::preload_rmed_wide})
+    if (f() != hipSuccess) (void)hipGetLastError();  // only an optimisation: the launch loads it otherwise
+  int rc;
+  if ((rc = d.stage.reserve(Impl::kStageChunk))) return rc;
+  // a small copy each way (the runtime's copy kernels) and a large one (its
+  // DMA engine path: the first 2 MB series upload took ~8 ms more than later ones)
+  DevBuf<uint8_t> probe;
+  constexpr size_t kLarge = 4u << 20;
+  if ((rc = probe.alloc(kLarge))) return rc;
+  std::memset(d.stage.p, 0, kLarge);
+  for (size_t n : {size_t{64}, kLarge}) {
+    BRP_HIP_CHECK(copy_sync(probe.p, d.stage.p, n, hipMemcpyHostToDevice, d.stream), RADPUL_HIP_MEM_COPY_HOST_DEVICE);
+    BRP_HIP_CHECK(copy_sync(d.stage.p, probe.p, n, hipMemcpyDeviceToHost, d.stream), RADPUL_HIP_MEM_COPY_DEVICE_HOST);
+  }
+  return 0;
+}
+
 int HipEngine::setup(const SearchGeometry& g, const std::vector<float>& series, float mu0) {
   if (series.size() < g.n_unpadded) return RADPUL_EVAL;
   return setup_impl(g, series.data(), nullptr, -1, mu0);
@@ -1347,7 +1374,8 @@ int HipEngine::setup_impl(const SearchGeometry& g, const float* host_series, con
     Impl::BatchIO& o = d.io[i];
     o.pending = false;
     if ((rc = o.in.alloc(in_bytes, d.fg_in))) return rc;
-    uint8_t* in_host = d.fg_in ? static_cast<uint8_t*>(host_view(d.device, o.in.p, in_bytes, d.stream)) : nullptr;
+    uint8_t* in_host =
+        d.fg_in ? static_cast<uint8_t*>(host_view(d.device, o.in.p, in_bytes, d.stream, d.stage)) : nullptr;
     if (d.fg_in && in_host == nullptr) {
       log_message(LOG_WARN, true, "Fine-grained device memory is not host visible; copying the batch parameters.\n");
       d.fg_in = false;
@@ -1362,7 +1390,8 @@ int HipEngine::setup_impl(const SearchGeometry& g, const float* host_series, con
       o.h_in_p = o.h_in.p;
     }
     uint2* cands_host =
-        d.fg_out ? static_cast<uint2*>(host_view(d.device, o.cands.p, sizeof(uint2) * (1 + d.kcopy), d.stream)) : nullptr;
+        d.fg_out ? static_cast<uint2*>(host_view(d.device, o.cands.p, sizeof(uint2) * (1 + d.kcopy), d.stream, d.stage))
+                 : nullptr;
     if (d.fg_out && cands_host == nullptr) {
       log_message(LOG_WARN, true, "Fine-grained device memory is not host visible; copying the results.\n");
       d.fg_out = false;
@@ -2120,6 +2149,7 @@ class HipBackend final : public Backend {
     return rc;
   }
   int device() const override { return eng_.device(); }
+  int warm_up() override { return eng_.warm_up(); }
   int preferred_batch() const override { return eng_.batch(); }
   BackendStats stats() const override { return eng_.stats(); }
 

@@ -72,6 +72,8 @@ class HipEngine {
   // the pruned harmonic sum's 8-bin bound cells of template k of the last
   // batch ((ps_stride >> 3) + 8 entries)
   int bound_cells(int k, std::vector<float>& cells);
+  // the first work's one-time costs ahead of it (code objects, copy kernels, stage)
+  int warm_up();
   // time each pipeline stage (prologue, pass1, pass2, pass3, harmonic, epilogue,
   // whole batch) over `reps` back-to-back launches on one batch; microseconds
   int benchmark_stages(const TemplateInput* t, int n, int reps, std::vector<double>& us_per_launch);

@@ -207,6 +207,11 @@ __global__ void __launch_bounds__(kThreads) bs_rows_kernel(const float2* H, floa
 
 }  // namespace
 
+hipError_t preload_bluestein() {
+  hipFuncAttributes at;
+  return hipFuncGetAttributes(&at, reinterpret_cast<const void*>(&bs_rows_kernel));
+}
+
 hipError_t launch_bs_rows(const float2* H, float2* hp, uint32_t L1, uint32_t L2, uint32_t L3, hipStream_t s) {
   const uint32_t n = L1 * L2 * L3;
   BRP_LAUNCH(bs_rows_kernel, dim3((n + kThreads - 1) / kThreads), dim3(kThreads), 0, s, H, hp, L1, L2, L3);

@@ -167,6 +167,15 @@ hipError_t launch_pass3_mid(const FFTPlan3& plan, const Pass3MidArgs& a, int bat
 // lengths of the transposed chirp-z convolution (pass3_mid, pass 2 rev, P1_REV_CHIRP)
 bool chirp_rev_supported(const FFTPlan3& plan);
 
+// code objects of the device modules onto the current device (each module's
+// is otherwise loaded at its first launch); HipEngine::warm_up
+hipError_t preload_fft_passes();
+hipError_t preload_harmonic_sum();
+hipError_t preload_whiten();
+hipError_t preload_resample();
+hipError_t preload_bluestein();
+hipError_t preload_rmed_wide();
+
 // lengths with compiled kernels
 bool pass12_length_supported(uint32_t L);
 bool pass3_length_supported(uint32_t L);

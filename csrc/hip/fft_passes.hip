@@ -1702,6 +1702,13 @@ hipError_t launch_pass3_mid(const FFTPlan3& plan, const Pass3MidArgs& a, int bat
   return launch_status();
 }
 
+// the module's code object onto the current device (loaded lazily at the
+// first launch otherwise: ~14 ms inside the first template batch, round 6)
+hipError_t preload_fft_passes() {
+  hipFuncAttributes at;
+  return hipFuncGetAttributes(&at, reinterpret_cast<const void*>(&pass3_kernel<256, kRowsP, P3_POWER>));
+}
+
 hipError_t launch_pass3_plain(const FFTPlan3& plan, const Pass3PlainArgs& a, hipStream_t s) {
   const dim3 grid(plan.wg3_plain());
   switch (plan.L3) {

@@ -838,6 +838,11 @@ __global__ void __launch_bounds__(256) hs_sel_emit_kernel(HSArgs a, HsSelectArgs
 
 }  // namespace
 
+hipError_t preload_harmonic_sum() {
+  hipFuncAttributes at;
+  return hipFuncGetAttributes(&at, reinterpret_cast<const void*>(&hs_sel_init_kernel));
+}
+
 uint32_t hs_num_blocks(int32_t i_start, uint32_t hhi) {
   const int64_t span = static_cast<int64_t>(hhi) - i_start;
   if (span <= 0) return 0;

@@ -60,6 +60,11 @@ __global__ void resample_kernel(const float* series, uint32_t n_unpadded, const 
 
 }  // namespace
 
+hipError_t preload_resample() {
+  hipFuncAttributes at;
+  return hipFuncGetAttributes(&at, reinterpret_cast<const void*>(&nsteps_kernel));
+}
+
 hipError_t launch_nsteps(TemplateDev* tmpl, int batch, hipStream_t s, uint32_t* reset) {
   BRP_LAUNCH(nsteps_kernel, dim3(batch), dim3(kThreads), 0, s, tmpl, reset);
   return launch_status();

@@ -291,6 +291,11 @@ size_t running_median_wide_scratch_bytes(uint32_t n_in) {
   return sizeof(uint32_t) * (5ull * n_in + 256ull * nblocks + 64);
 }
 
+hipError_t preload_rmed_wide() {
+  hipFuncAttributes at;
+  return hipFuncGetAttributes(&at, reinterpret_cast<const void*>(&rs_init));
+}
+
 hipError_t launch_running_median_wide(const float* in, uint32_t n_in, uint32_t W, float* med, void* scratch,
                                       hipStream_t s) {
   if (W == 0 || n_in < W || scratch == nullptr) return hipErrorInvalidValue;

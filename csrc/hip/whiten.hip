@@ -323,6 +323,11 @@ __global__ void tangle_kernel(const float2* spec, uint32_t M, uint32_t fft_size,
 
 }  // namespace
 
+hipError_t preload_whiten() {
+  hipFuncAttributes at;
+  return hipFuncGetAttributes(&at, reinterpret_cast<const void*>(&whiten_power_kernel));
+}
+
 hipError_t launch_unpack(const uint8_t* packed, uint32_t n_packed, bool four_bit, double scale, float* out,
                          uint32_t n_out, hipStream_t s) {
   if (n_out == 0) return hipSuccess;
