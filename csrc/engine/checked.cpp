@@ -202,9 +202,12 @@ void chk_unregister(const void* p) {
 }
 
 void chk_before_launch(hipStream_t s) {
-  (void)s;
   Registry& r = reg();
   r.launch_mu.lock();  // released by chk_after_launch (BRP_LAUNCH pairs them)
+  // a launch being captured into a graph runs later: no device-wide work now
+  // (a synchronisation would invalidate the capture)
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) return;
   hipError_t e = ensure_bound(r);
   if (e == hipSuccess) e = upload(r);
   if (e != hipSuccess) {
