@@ -201,6 +201,61 @@ def build_asan(force: bool = False, jobs: int | None = None, verbose: bool = Tru
     return app
 
 
+OBJ_TSAN = ROOT / "build" / "obj_tsan"
+
+
+def tsan_app_path() -> Path:
+    return BIN / "einsteinbinary_mi355x_tsan"
+
+
+def build_tsan(force: bool = False, jobs: int | None = None, verbose: bool = True) -> Path:
+    """ThreadSanitizer build of the application (SURVEY.md 5.2 race detection):
+    every host translation unit instrumented; the device modules' objects are
+    the product build's (their host side is only kernel stubs and launchers,
+    which the CPU backend never calls)."""
+    jobs = jobs or min(16, os.cpu_count() or 4)
+    hdr = _headers_mtime()
+    prod = build(force=False, jobs=jobs, verbose=False)  # the device objects
+    del prod
+    srcs = HOST_SRCS + [APP_MAIN]
+
+    def comp(src_rel: str) -> tuple[str, Path]:
+        src = CSRC / src_rel
+        obj = OBJ_TSAN / (src_rel.replace("/", "__") + ".o")
+        if not _needs(obj, src, hdr, force):
+            return "cached", obj
+        obj.parent.mkdir(parents=True, exist_ok=True)
+        flags = [f for f in _common_flags() if f != "-O3"] + ["-O1", "-g", "-fsanitize=thread", "-fno-omit-frame-pointer"]
+        cmd = [CLANG, *flags, "-c", str(src), "-o", str(obj)]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"compile failed: {src_rel}\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+        return "built", obj
+
+    results = {}
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        futs = {ex.submit(comp, s): s for s in srcs}
+        for f in cf.as_completed(futs):
+            status, obj = f.result()
+            results[futs[f]] = obj
+            if verbose and status == "built":
+                print(f"[build tsan] {futs[f]}", flush=True)
+    objs = [results[s] for s in HOST_SRCS] + [OBJ / (s.replace("/", "__") + ".o") for s in DEVICE_SRCS]
+    objs.append(results[APP_MAIN])
+    app = tsan_app_path()
+    if force or not app.exists() or app.stat().st_mtime < max(o.stat().st_mtime for o in objs):
+        out = app.with_name(app.name + ".tmp")
+        cmd = [HIPCC, f"--offload-arch={ARCH}", *[str(o) for o in objs], "-o", str(out), f"-L{ROCM / 'lib'}",
+               "-lamdhip64", "-lz", "-lpthread", "-ldl", "-fsanitize=thread", f"-Wl,-rpath,{ROCM / 'lib'}"]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed: {app}\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+        os.replace(out, app)
+        if verbose:
+            print(f"[build tsan] linked {app.relative_to(ROOT)}", flush=True)
+    return app
+
+
 def build_checked(force: bool = False, jobs: int | None = None, verbose: bool = True) -> dict:
     """Device-side debug build (csrc/hip/checked.hpp): module _brp_checked and
     bin/einsteinbinary_mi355x_checked."""
@@ -236,12 +291,15 @@ def main(argv=None) -> int:
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", "--jobs", type=int, default=None)
     ap.add_argument("--asan", action="store_true", help="also build bin/einsteinbinary_mi355x_asan (ASan + UBSan)")
+    ap.add_argument("--tsan", action="store_true", help="also build bin/einsteinbinary_mi355x_tsan (ThreadSanitizer)")
     ap.add_argument("--checked", action="store_true",
                     help="also build the device-side debug build (_brp_checked, bin/einsteinbinary_mi355x_checked)")
     a = ap.parse_args(argv)
     out = build(force=a.force, jobs=a.jobs)
     if a.asan:
         out["asan_app"] = str(build_asan(force=a.force, jobs=a.jobs))
+    if a.tsan:
+        out["tsan_app"] = str(build_tsan(force=a.force, jobs=a.jobs))
     if a.checked:
         out.update(build_checked(force=a.force, jobs=a.jobs))
     print(out)

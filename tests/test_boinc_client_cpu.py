@@ -222,3 +222,37 @@ def test_kill_signals_ignored_three_times(app, case, tmp_path):
     assert "Got 4th kill-signal" in err
     assert (tmp_path / "boinc_finish_called").read_text().strip() == "0"
     assert not (tmp_path / "result.cand").exists()
+
+
+def test_tsan_under_client_suspend_resume_quit(case, reference_result, tmp_path):
+    """Race detection with the client in the loop: the ThreadSanitizer build
+    (_build.py --tsan) with two CPU workers, the runtime's status / control
+    thread and the fake client's suspend, resume, then quit and restart. No
+    ThreadSanitizer report, and the restarted task finishes with the
+    uninterrupted result."""
+    from boinc_app_eah_brp_amd import _build
+
+    tsan = _build.build_tsan(verbose=False)
+    env = _slow_env(TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1")
+    slot = tmp_path / "slot"
+    cl = FakeClient(slot)
+    try:
+        cl.start(_args(tsan, case, ("--mi355x-gpus", "2")), env=env)
+        cl.wait_fraction(0.2)
+        cl.control("<suspend/>")
+        time.sleep(0.6)
+        cl.control("<resume/>")
+        cl.wait_fraction(0.4)
+        cl.control("<quit/>")
+        rc, out, err = cl.wait(timeout=120)
+    finally:
+        cl.close()
+    assert rc == 0 and "ThreadSanitizer" not in err, err[-6000:]
+    cl2 = FakeClient(slot)
+    try:
+        cl2.start(_args(tsan, case, ("--mi355x-gpus", "2")), env=dict(env, BRP_FAULT="slow_template:5"))
+        rc, out, err = cl2.wait(timeout=180)
+    finally:
+        cl2.close()
+    assert rc == 0 and "ThreadSanitizer" not in err, err[-6000:]
+    assert _cands(slot / "result.cand") == reference_result
