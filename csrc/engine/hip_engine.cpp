@@ -490,6 +490,8 @@ struct HipEngine::Impl {
   // profiles/README.md round 6)
   bool p3_cells = false;
   bool fused_cells() const { return p3_cells && hs_prune && hs_cell_shift == 3 && !bs; }
+  // 8-bin cells per thread of the fp32 cell kernel (BRP_HS_CELLS_CPT: 1 or 4)
+  uint32_t hs_cells_cpt = 1;
   bool hs_direct = true;        // bounds read straight from global memory (BRP_HS_DIRECT=0: LDS-staged;
                                 // +2 % fp32, +3 % config 5 in one call, profiles/README.md round 3)
   DevBuf<double> partials;      // [batch][wg1]
@@ -957,6 +959,7 @@ struct HipEngine::Impl {
         ah.pyr = pyr.p;
         ah.pyr_stride = hipk::hs_pyr_stride(ps_stride);
         ah.cells_ready = !bs && fused_cells();  // pass 3 wrote the own-bin cells
+        ah.cells_cpt = hs_cells_cpt;
         ah.row_c = plan.L1 * plan.L2;
         ah.row_l = plan.L3;
         ah.key_base = key_base;
@@ -1342,6 +1345,7 @@ int HipEngine::setup_impl(const SearchGeometry& g, const float* host_series, con
     d.inplace_max = std::min<uint32_t>(d.kcopy, static_cast<uint32_t>(std::max(0, std::atoi(e))));
   d.hs_direct = std::getenv("BRP_HS_DIRECT") == nullptr || std::atoi(std::getenv("BRP_HS_DIRECT")) != 0;
   d.p3_cells = std::getenv("BRP_P3_CELLS") != nullptr && std::atoi(std::getenv("BRP_P3_CELLS")) != 0;
+  d.hs_cells_cpt = (std::getenv("BRP_HS_CELLS_CPT") && std::atoi(std::getenv("BRP_HS_CELLS_CPT")) == 4) ? 4u : 1u;
   d.hs_xcd = std::getenv("BRP_HS_XCD") != nullptr && std::atoi(std::getenv("BRP_HS_XCD")) == 1;
   d.lds_pass1 = std::getenv("BRP_P1_LDS") != nullptr && std::atoi(std::getenv("BRP_P1_LDS")) == 1;
   d.mid_waves = std::getenv("BRP_MID_WAVES") != nullptr && std::atoi(std::getenv("BRP_MID_WAVES")) == 1;

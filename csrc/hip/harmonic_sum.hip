@@ -262,6 +262,49 @@ __global__ void __launch_bounds__(256) hs_cells_kernel(HSArgs a) {
          v[0]);
 }
 
+// 8-bin cells of an fp32 spectrum, CPT cells per thread (cells m0 + 256 j):
+// all 2 CPT float4 loads are issued before the first maximum (one wave keeps
+// 8 KB in flight instead of 2 KB; the one-cell kernel spent 81 % of its wave
+// time waiting, profiles/hs_pmc_r6.txt). Cells reaching past hhi take the
+// guarded per-bin path; their unconditional loads read bin 0 instead.
+template <int CPT>
+__global__ void __launch_bounds__(256) hs_cells8_kernel(HSArgs a) {
+  const int b = blockIdx.y;
+  const uint32_t n = (a.ps_stride >> 3) + 8;
+  const uint32_t m0 = blockIdx.x * (256u * CPT) + threadIdx.x;
+  const float* P = a.ps + static_cast<size_t>(b) * a.ps_stride;
+  float4 x[CPT][2];
+#pragma unroll
+  for (int j = 0; j < CPT; ++j) {
+    const uint32_t m = m0 + 256u * j, k0 = 8u * m;
+    const uint32_t ks = (m < n && k0 + 8 <= a.hhi) ? k0 : 0u;
+    x[j][0] = BRP_LD(reinterpret_cast<const float4*>(P + ks));
+    x[j][1] = BRP_LD(reinterpret_cast<const float4*>(P + ks) + 1);
+  }
+#pragma unroll
+  for (int j = 0; j < CPT; ++j) {
+    const uint32_t m = m0 + 256u * j, k0 = 8u * m;
+    if (m >= n) break;
+    float v;
+    if (k0 + 8 <= a.hhi) {
+      v = fmaxf(fmaxf(fmaxf(x[j][0].x, x[j][1].x), fmaxf(x[j][0].y, x[j][1].y)),
+                fmaxf(fmaxf(x[j][0].z, x[j][1].z), fmaxf(x[j][0].w, x[j][1].w)));
+    } else {
+      float t[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) t[e] = (k0 + e < a.hhi) ? BRP_LD(&P[k0 + e]) : 0.0f;
+#pragma unroll
+      for (int w = 4; w >= 1; w /= 2)
+#pragma unroll
+        for (int e = 0; e < w; ++e) t[e] = fmaxf(t[e], t[e + w]);
+      v = t[0];
+    }
+    BRP_ST(&a.pyr[BRP_INJECT_AT(static_cast<size_t>(b) * a.pyr_stride + m,
+                                static_cast<size_t>(gridDim.y) * a.pyr_stride + 16, kInjHsCells)],
+           v);
+  }
+}
+
 // harmonics in the reference summation order, their source (0: spectrum,
 // CK: 2^CK-bin cells) and their slice of a wave's staging buffer
 constexpr int kHarm[16] = {16, 8, 12, 4, 14, 10, 6, 2, 15, 13, 11, 9, 7, 5, 3, 1};
@@ -863,10 +906,11 @@ hipError_t launch_harmonic_sum(const HSArgs& a, int batch, hipStream_t s) {
     // cells pass 3 left (cells_ready): the mirror half of rows k3 < L3, then the cells from M/8 on
     const uint32_t n8 = (a.ps_stride >> 3) + 8, m8 = (a.row_c >> 3) * a.row_l;
     const uint32_t n_rest = (a.row_c >> 4) * a.row_l + (n8 > m8 ? n8 - m8 : 0u);
-    const dim3 gr((n_rest + 255) / 256, batch);
+    const dim3 gr((n_rest + 255) / 256, batch), g4((n8 + 1023) / 1024, batch);
 #define BRP_HS_PRUNED(CK, MODE, DIRECT)                                                    \
   do {                                                                                    \
     if (CK == 3 && a.cells_ready) BRP_LAUNCH((hs_cells_kernel<CK, MODE, true>), gr, dim3(256), 0, s, a); \
+    else if (CK == 3 && MODE == HS_F32 && a.cells_cpt == 4) BRP_LAUNCH(hs_cells8_kernel<4>, g4, dim3(256), 0, s, a); \
     else BRP_LAUNCH((hs_cells_kernel<CK, MODE>), gc, dim3(256), 0, s, a);                \
     BRP_LAUNCH((hs_pruned_kernel<CK, MODE, DIRECT>), gp, dim3(256), 0, s, a, nblk);       \
   } while (0)

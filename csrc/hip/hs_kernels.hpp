@@ -42,6 +42,7 @@ struct HSArgs {
   // cell kernel computes only the others (mirror half and past M)
   bool cells_ready;
   uint32_t row_c, row_l;
+  uint32_t cells_cpt;  // fp32 8-bin cells per thread of the cell kernel (1: hs_cells_kernel, 4: hs_cells8_kernel<4>)
   uint32_t key_base;  // index of template 0 of this launch within the batch's candidate list
   uint32_t bin_bits;  // candidate key layout (hs_pack): bins < 2^bin_bits
   float* dense;       // select path: [batch][5][dense_stride] level values (HsSelectArgs)

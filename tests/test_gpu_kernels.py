@@ -134,15 +134,16 @@ def _host_cells(ps, geom, n):
     return v.reshape(n, 8).max(axis=1)
 
 
-@pytest.mark.parametrize("p3cells", ["0", "1"])
+@pytest.mark.parametrize("cells", ["hs_cells", "hs_cells8", "p3"])
 @pytest.mark.parametrize("case", ["bench", "small"])
-def test_bound_cells_equal_spectrum_maxima(brp, gpu, tmp_path, monkeypatch, case, p3cells):
-    """The pruned harmonic sum's 8-bin bound cells (hs_cells_kernel; with
-    BRP_P3_CELLS=1 the own-bin cells from pass 3 and the mirror half from
-    hs_cells_kernel) equal the 8-bin maxima of the spectrum pass 3 stored, bit
-    for bit, zero beyond the harmonic range (the bounds' monotonicity argument
-    needs cells >= every bin)."""
-    monkeypatch.setenv("BRP_P3_CELLS", p3cells)
+def test_bound_cells_equal_spectrum_maxima(brp, gpu, tmp_path, monkeypatch, case, cells):
+    """The pruned harmonic sum's 8-bin bound cells (hs_cells_kernel; 4 cells
+    per thread with BRP_HS_CELLS_CPT=4; with BRP_P3_CELLS=1 the own-bin cells
+    from pass 3 and the mirror half from hs_cells_kernel) equal the 8-bin
+    maxima of the spectrum pass 3 stored, bit for bit, zero beyond the harmonic
+    range (the bounds' monotonicity argument needs cells >= every bin)."""
+    monkeypatch.setenv("BRP_P3_CELLS", "1" if cells == "p3" else "0")
+    monkeypatch.setenv("BRP_HS_CELLS_CPT", "4" if cells == "hs_cells8" else "1")
     opt = None
     if case == "bench":
         hdr, series, _ = brp.read_work_unit(str(WU))
