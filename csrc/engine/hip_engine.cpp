@@ -254,6 +254,17 @@ hipError_t memcpy_async(void* dst, const void* src, size_t bytes, hipMemcpyKind 
   return hipMemcpyAsync(dst, src, bytes, kind, s);
 }
 
+// page-locked host memory the runtime knows (hipHostMalloc, hipHostRegister):
+// copies may read / write it directly
+bool host_pinned(const void* p) {
+  hipPointerAttribute_t at{};
+  if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return at.type == hipMemoryTypeHost;
+}
+
 hipError_t copy_sync(void* dst, const void* src, size_t bytes, hipMemcpyKind kind, hipStream_t s) {
   const hipError_t e = memcpy_async(dst, src, bytes, kind, s);
   if (e != hipSuccess) return e;
@@ -564,6 +575,7 @@ struct HipEngine::Impl {
   static constexpr size_t kStageChunk = 8u << 20;
   hipError_t copy_out(void* dst, const void* src, size_t bytes) {
     if (bytes == 0) return hipSuccess;
+    if (host_pinned(dst)) return copy_sync(dst, src, bytes, hipMemcpyDeviceToHost, stream);  // caller's pinned buffer
     if (stage.reserve(std::min(bytes, kStageChunk))) return hipErrorOutOfMemory;
     for (size_t off = 0; off < bytes; off += kStageChunk) {
       const size_t nb = std::min(kStageChunk, bytes - off);
@@ -576,6 +588,8 @@ struct HipEngine::Impl {
   }
   hipError_t copy_in(void* dst, const void* src, size_t bytes) {
     if (bytes == 0) return hipSuccess;
+    // a registered source (the WU buffers search.cpp / multi.cpp page-lock) is read directly
+    if (host_pinned(src)) return copy_sync(dst, src, bytes, hipMemcpyHostToDevice, stream);
     if (stage.reserve(std::min(bytes, kStageChunk))) return hipErrorOutOfMemory;
     for (size_t off = 0; off < bytes; off += kStageChunk) {
       const size_t nb = std::min(kStageChunk, bytes - off);
