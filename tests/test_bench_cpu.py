@@ -1,5 +1,5 @@
 """The driver-facing bench.py contract on CPU: launched by torch.distributed.run
-with 2 and 4 ranks (gloo, CPU golden backend, small synthetic WU via --cpu),
+with 2, 4 and 8 ranks (8: the driver's N=8 shape) (gloo, CPU golden backend, small synthetic WU via --cpu),
 rank 0 prints exactly one JSON line with the whole-job value, and the sharded,
 all-gathered result file equals the single-rank one byte for byte."""
 import json
@@ -32,7 +32,7 @@ def _bench(nproc, tmp, out):
     return json.loads(lines[0])
 
 
-@pytest.mark.parametrize("nproc", [2, 4])
+@pytest.mark.parametrize("nproc", [2, 4, 8])
 def test_bench_multirank_cpu_rehearsal(nproc, tmp_path):
     one = _bench(1, tmp_path / "w1", tmp_path / "one.cand")
     many = _bench(nproc, tmp_path / f"w{nproc}", tmp_path / "many.cand")

@@ -123,22 +123,22 @@ def _bench_json(args, env_extra, tmp):
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
     env.update(TMPDIR=str(tmp), BRP_NO_RESULT_HEADER="1", **env_extra)
     r = subprocess.run([sys.executable, "bench.py", *args], cwd=ROOT, env=env, capture_output=True, text=True,
-                       timeout=110)
+                       timeout=170)
     assert r.returncode == 0, r.stderr[-4000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]
     return json.loads(lines[0])
 
 
-@pytest.mark.parametrize("nranks", [2, 4])
+@pytest.mark.parametrize("nranks", [2, 4, 8])
 def test_bench_self_launched_ranks_on_one_gpu(gpu, tmp_path, nranks):
     """`bench.py --gpus N` through its own launcher (launch_ranks: N Popen'd
     rank processes, the floor exchange during the step, the all-gather and the
     merge) with BRP_BENCH_SHARE_DEVICE=1, so that all ranks run on this box's
     one GPU over gloo: the table equals the one-rank run's byte for byte. With
-    4 ranks FloorSync's all-reduce has more than two members (the 8-GPU node's
-    first run is otherwise its first execution at that size). No throughput is
-    taken from it (the JSON line says so)."""
+    4 and 8 ranks FloorSync's all-reduce has more than two members; 8 is the
+    driver's 8-GPU shape (whose first run is otherwise its first execution at
+    that size). No throughput is taken from it (the JSON line says so)."""
     common = ["--templates", "200", "--steps", "1", "--warmup", "1"]
     one = _bench_json(["--gpus", "1", *common, "--write-output", str(tmp_path / "one.cand")], {}, tmp_path)
     many = _bench_json(["--gpus", str(nranks), *common, "--write-output", str(tmp_path / "many.cand")],
