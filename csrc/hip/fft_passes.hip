@@ -459,8 +459,11 @@ __global__ void __launch_bounds__(kNcol * tpc_for<L>(), kMinWaves) pass2_kernel(
 // times, with two barriers per tile. The output twiddle
 // W_M^{n3 (k1 + L1 k2)} = wc * W_{L2L3}^{n3 tj} * (W_{L2L3}^{n3 TPC})^q is
 // evaluated exactly at q = 0 and q = 8 and stepped by one rotation in between.
+#ifndef BRP_P2R_WAVES
+#define BRP_P2R_WAVES 3  // minimum waves per SIMD the register budget must allow (build switch)
+#endif
 template <int L, bool REV = false>
-__global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_per_eu(3, 8))) pass2r_kernel(Pass2Args a, uint32_t ntiles) {
+__global__ void __launch_bounds__(kNcol * (L / 16)) __attribute__((amdgpu_waves_per_eu(BRP_P2R_WAVES, 8))) pass2r_kernel(Pass2Args a, uint32_t ntiles) {
   constexpr int R1 = L / 16;
   constexpr int TPC = R1;
   constexpr int NT = kNcol * TPC;
