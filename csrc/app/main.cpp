@@ -10,9 +10,11 @@
 #include "search.hpp"
 
 int main(int argc, char** argv) {
+  brp::trace::phase("main");
   brp::log_message(brp::LOG_INFO, true, "Application startup - thank you for supporting Einstein@Home!\n");
   brp::log_message(brp::LOG_DEBUG, true, "Setting up diagnotics and exception handling...\n");
   brp::crash::install();
+  brp::trace::phase("crash handlers");
   brp::log_message(brp::LOG_DEBUG, true, "Initializing BOINC...\n");
   brp::boinc::init(argc, argv);
   brp::trace::phase("boinc runtime init");

@@ -6,14 +6,17 @@
 #include <fcntl.h>
 #include <link.h>
 #include <signal.h>
+#include <time.h>
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../core/errors.hpp"
@@ -35,8 +38,15 @@ struct Module {
   char name[128];
 };
 
-std::vector<Sym> g_syms;
-std::string g_names;
+// The executable's function symbols, read and demangled on a thread started
+// by install() (16-20 ms for this binary, which would otherwise delay the HIP
+// runtime start behind it) and published whole: a crash before then prints
+// module offsets only. Never freed (the loader may still run at exit).
+struct SymTable {
+  std::vector<Sym> syms;
+  std::string names;
+};
+std::atomic<const SymTable*> g_tab{nullptr};
 uintptr_t g_exe_bias = 0;
 uintptr_t g_exe_lo = 0, g_exe_hi = 0;
 constexpr int kMaxModules = 128;
@@ -112,6 +122,13 @@ int collect_module(struct dl_phdr_info* info, size_t, void*) {
 }
 
 void load_symbols() {
+  auto* tab = new SymTable;
+  std::vector<Sym>& g_syms = tab->syms;
+  std::string& g_names = tab->names;
+  struct Publish {
+    SymTable* t;
+    ~Publish() { g_tab.store(t, std::memory_order_release); }  // an empty table too
+  } publish{tab};
   FILE* f = std::fopen("/proc/self/exe", "rb");
   if (!f) return;
   std::vector<char> img;
@@ -156,7 +173,9 @@ void load_symbols() {
 }
 
 // lookup without allocation: binary search over the sorted table
-const Sym* find_sym(uintptr_t link_addr) {
+const Sym* find_sym(const SymTable* tab, uintptr_t link_addr) {
+  if (tab == nullptr) return nullptr;
+  const std::vector<Sym>& g_syms = tab->syms;
   size_t lo = 0, hi = g_syms.size();
   while (lo < hi) {
     const size_t mid = (lo + hi) / 2;
@@ -174,10 +193,11 @@ void put_frame(int k, void* pc) {
   put_dec(k);
   put(" ");
   put_hex(a);
+  const SymTable* tab = g_tab.load(std::memory_order_acquire);
   if (a >= g_exe_lo && a < g_exe_hi) {
-    if (const Sym* s = find_sym(a - g_exe_bias)) {
+    if (const Sym* s = find_sym(tab, a - g_exe_bias)) {
       put(" in ");
-      put(g_names.c_str() + s->name);
+      put(tab->names.c_str() + s->name);
       put("+");
       put_hex(a - g_exe_bias - s->lo);
       put("\n");
@@ -211,6 +231,12 @@ void handler(int sig, siginfo_t*, void*) {
     }
     return;
   }
+  // a crash while the symbol loader still runs waits for it (up to 2 s;
+  // nanosleep is async-signal-safe, the loader is another thread)
+  for (int w = 0; w < 200 && g_tab.load(std::memory_order_acquire) == nullptr; ++w) {
+    const struct timespec ts{0, 10 * 1000 * 1000};
+    nanosleep(&ts, nullptr);
+  }
   void* frames[64];
   const int n = backtrace(frames, 64);
   put("\nObtained ");
@@ -230,7 +256,7 @@ void install() {
   backtrace(warm, 2);  // loads the unwinder now, not inside the handler
   g_nmods = 0;
   dl_iterate_phdr(collect_module, nullptr);
-  load_symbols();
+  std::thread(load_symbols).detach();
   const int fd = dup(2);
   if (fd >= 0) g_fd = fd;
   if (const char* s = std::getenv("BRP_CRASH_SLEEP")) g_sleep_s = static_cast<unsigned>(std::atoi(s));
@@ -244,9 +270,10 @@ void install() {
 
 bool describe(const void* addr, char* out, int out_size) {
   const uintptr_t a = reinterpret_cast<uintptr_t>(addr);
+  const SymTable* tab = g_tab.load(std::memory_order_acquire);
   if (a >= g_exe_lo && a < g_exe_hi) {
-    if (const Sym* s = find_sym(a - g_exe_bias)) {
-      std::snprintf(out, out_size, "%s", g_names.c_str() + s->name);
+    if (const Sym* s = find_sym(tab, a - g_exe_bias)) {
+      std::snprintf(out, out_size, "%s", tab->names.c_str() + s->name);
       return true;
     }
   }
