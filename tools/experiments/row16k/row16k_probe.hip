@@ -1,0 +1,317 @@
+// Probe of a two-pass real-column plan for the benchmark's 3 * 2^22-point
+// real FFT (round 6): N = 768 * 16384. Pass A would transform the real
+// columns (length 768, the first third non-zero) and keep the 385 rows
+// k1 = 0 .. 384 (the others are their conjugates); pass B, probed here,
+// transforms each row of 16384 complex points in ONE workgroup (LDS-resident,
+// 139 KB) and writes its power row, so no row needs a partner row and the
+// three-pass plan's pass 2 (a 50 MB read + write per template) disappears.
+//
+//   rowfft16k: 1024 threads x 16 points, radix 16 | 16 | 16 | 4 (the last
+//              radix across lane quads), power row staged in LDS and written
+//              with float4 stores
+//   copy     : float4 streaming copy of the same bytes (50.5 MB in, 25 MB out)
+//
+// Checked against a double-precision DFT of a few rows; us per template
+// (385 rows) single stream, 1 and 3 templates per launch.
+// Build: hipcc --offload-arch=gfx950 -O3 row16k_probe.hip -o row16k_probe
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CHECK(x)                                                               \
+  do {                                                                         \
+    hipError_t e_ = (x);                                                       \
+    if (e_ != hipSuccess) {                                                    \
+      std::printf("HIP error %s at line %d\n", hipGetErrorName(e_), __LINE__); \
+      std::exit(1);                                                            \
+    }                                                                          \
+  } while (0)
+
+constexpr int kL = 16384;
+constexpr int kRows = 385;
+constexpr int kNT = 1024;
+
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+  return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ float2 mul_mi(float2 a) { return make_float2(a.y, -a.x); }
+
+// in-register DFT-4 / DFT-16 (forward, W = exp(-2 pi i / n))
+__device__ __forceinline__ void dft4(float2& a, float2& b, float2& c, float2& d) {
+  const float2 s0 = cadd(a, c), d0 = csub(a, c), s1 = cadd(b, d), d1 = mul_mi(csub(b, d));
+  a = cadd(s0, s1);
+  c = csub(s0, s1);
+  b = cadd(d0, d1);
+  d = csub(d0, d1);
+}
+__device__ __forceinline__ void dft16(float2* v) {
+  // 4 x 4: columns (stride 4), twiddle W_16^{r c}, rows
+#pragma unroll
+  for (int r = 0; r < 4; ++r) dft4(v[r], v[r + 4], v[r + 8], v[r + 12]);
+  const float c1 = 0.92387953251128674f, s1 = 0.38268343236508978f, h = 0.70710678118654752f;
+  const float2 w1 = make_float2(c1, -s1), w2 = make_float2(h, -h), w3 = make_float2(s1, -c1);
+  v[5] = cmul(v[5], w1);
+  v[6] = cmul(v[6], w2);
+  v[7] = cmul(v[7], w3);
+  v[9] = cmul(v[9], w2);
+  v[10] = mul_mi(v[10]);
+  v[11] = cmul(v[11], make_float2(-h, -h));
+  v[13] = cmul(v[13], w3);
+  v[14] = cmul(v[14], make_float2(-h, -h));
+  v[15] = cmul(v[15], make_float2(-c1, s1));
+  // v[r + 4 c] now holds column-transform output c of row... rows r: DFT over r
+#pragma unroll
+  for (int c = 0; c < 4; ++c) dft4(v[4 * c], v[4 * c + 1], v[4 * c + 2], v[4 * c + 3]);
+  // output k = c + 4 k' sits at v[4 c + k']: reorder to natural
+  float2 o[16];
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) o[c + 4 * kk] = v[4 * c + kk];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) v[i] = o[i];
+}
+
+
+#ifndef TW_MODE
+#define TW_MODE 1
+#endif
+// W_16384^{e k}: TW_MODE 0 one table load per twiddle (scattered lines),
+// 1: anchors at k = 1, 4, 8, 12 from the table, stepped by W^e in between;
+// 2: LDS tables (two-level W_16384 in stage 0, W_1024 in stages 1-2), in the kernel
+__device__ __forceinline__ float2 tw_at(const float2* __restrict__ w, int e, int k) {
+  if (TW_MODE == 0) return w[(e * k) & (kL - 1)];
+  const int a = k & ~3;
+  float2 r = w[(e * (a ? a : 1)) & (kL - 1)];
+  const float2 w1 = w[e & (kL - 1)];
+  for (int j = (a ? a : 1); j < k; ++j) r = cmul(r, w1);
+  return r;
+}
+
+// padded LDS index of complex element a (4 float2 every 64: stage-2 reads conflict-free)
+__device__ __forceinline__ int pidx(int a) { return a + 4 * (a >> 6); }
+// padded float index of power bin K
+__device__ __forceinline__ int fidx(int K) { return K + (K >> 4) + (K >> 12); }
+
+// W_16384^e table in global memory (L2 resident)
+__global__ void __launch_bounds__(kNT) rowfft16k(const float2* __restrict__ in, float* __restrict__ out,
+                                                 const float2* __restrict__ w16k) {
+  __shared__ float2 lds[kL + 4 * (kL / 64)];
+  __shared__ float2 t1k[1024], thi[128], tlo[128];  // W_1024^e, W_16384^{128 e}, W_16384^e
+  if (TW_MODE == 2) {
+    t1k[threadIdx.x] = w16k[16 * threadIdx.x];
+    if (threadIdx.x < 128) {
+      thi[threadIdx.x] = w16k[128 * threadIdx.x];
+      tlo[threadIdx.x] = w16k[threadIdx.x];
+    }
+    __syncthreads();
+  }
+  const int row = blockIdx.x;
+  const int b = blockIdx.y;
+  const float2* src = in + (static_cast<size_t>(b) * kRows + row) * kL;
+  const int t = threadIdx.x;
+  float2 v[16];
+  // stage 0: x[t + 1024 q] -> DFT16 over q -> k0; twiddle W_16384^{t k0}
+#pragma unroll
+  for (int q = 0; q < 16; ++q) v[q] = src[t + 1024 * q];
+  dft16(v);
+#pragma unroll
+  for (int k = 1; k < 16; ++k) {
+    if (TW_MODE == 2) { const int e = (t * k) & (kL - 1); v[k] = cmul(v[k], cmul(thi[e >> 7], tlo[e & 127])); }
+    else v[k] = cmul(v[k], tw_at(w16k, t, k));
+  }
+#pragma unroll
+  for (int k = 0; k < 16; ++k) lds[pidx(k * 1024 + t)] = v[k];
+  __syncthreads();
+  // stage 1: thread (k0, t1): A[k0][t1 + 64 q] -> k1; twiddle W_1024^{t1 k1}; in place
+  {
+    const int k0 = t >> 6, t1 = t & 63;
+    const int base = k0 * 1024 + t1;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) v[q] = lds[pidx(base + 64 * q)];
+    dft16(v);
+#pragma unroll
+    for (int k = 1; k < 16; ++k) v[k] = cmul(v[k], TW_MODE == 2 ? t1k[(t1 * k) & 1023] : tw_at(w16k, 16 * t1, k));
+#pragma unroll
+    for (int k = 0; k < 16; ++k) lds[pidx(base + 64 * k)] = v[k];
+  }
+  __syncthreads();
+  // stage 2: thread (k0, k1, t2): B[k0][k1][t2 + 4 q] -> k2; twiddle W_64^{t2 k2}
+  const int t2 = t & 3, k1 = (t >> 2) & 15, k0 = t >> 6;
+  {
+    const int base = k0 * 1024 + k1 * 64 + t2;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) v[q] = lds[pidx(base + 4 * q)];
+    dft16(v);
+#pragma unroll
+    for (int k = 1; k < 16; ++k) v[k] = cmul(v[k], TW_MODE == 2 ? t1k[(16 * t2 * k) & 1023] : tw_at(w16k, 256 * t2, k));
+  }
+  // stage 3: radix 4 across the lane quad (t2 = 2 b1 + b0): lane (b1, b0) ends with k3 = b1 + 2 b0
+  const int b1 = t2 >> 1, b0 = t2 & 1;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    float2 p;
+    p.x = __shfl_xor(v[k].x, 2);
+    p.y = __shfl_xor(v[k].y, 2);
+    float2 u = b1 ? csub(p, v[k]) : cadd(v[k], p);
+    if (b1 && b0) u = mul_mi(u);
+    p.x = __shfl_xor(u.x, 1);
+    p.y = __shfl_xor(u.y, 1);
+    v[k] = b0 ? csub(p, u) : cadd(u, p);
+  }
+  __syncthreads();  // LDS free: power row
+  float* pw = reinterpret_cast<float*>(lds);
+  const int k3 = b1 + 2 * b0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int K = k0 + 16 * k1 + 256 * k + 4096 * k3;
+    pw[fidx(K)] = v[k].x * v[k].x + v[k].y * v[k].y;
+  }
+  __syncthreads();
+  float* dst = out + (static_cast<size_t>(b) * kRows + row) * kL;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int K = 4 * t + 4096 * j;
+    const float4 o = make_float4(pw[fidx(K)], pw[fidx(K + 1)], pw[fidx(K + 2)], pw[fidx(K + 3)]);
+    reinterpret_cast<float4*>(dst)[K / 4] = o;
+  }
+}
+
+// memory shape of pass A (no arithmetic): a workgroup of 256 threads owns 16
+// adjacent columns n2; each thread reads the 16 samples of its 8 packed rows
+// (x[(2 m) 16384 + n2], x[(2 m + 1) 16384 + n2], m = tj + 16 q) and the
+// workgroup writes the 385 output rows of its columns (128-B row pieces)
+__global__ void __launch_bounds__(256) passA_shape(const float* __restrict__ series, float2* __restrict__ out) {
+  __shared__ float2 col[385 * 16];
+  const int c = threadIdx.x & 15, tj = threadIdx.x >> 4;
+  const int n2 = blockIdx.x * 16 + c;
+  const int b = blockIdx.y;
+  float v[16];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int m = tj + 16 * q;
+    v[2 * q] = series[(2 * m) * kL + n2];
+    v[2 * q + 1] = series[(2 * m + 1) * kL + n2];
+  }
+#pragma unroll
+  for (int q = 0; q < 8; ++q) col[(tj + 16 * q) * 16 + c] = make_float2(v[2 * q], v[2 * q + 1]);
+  __syncthreads();
+  float2* dst = out + static_cast<size_t>(b) * kRows * kL;
+  for (int r = tj; r < kRows; r += 16) {
+    const float2 z = col[(r % 128) * 16 + c];
+    dst[static_cast<size_t>(r) * kL + n2] = z;
+  }
+}
+
+__global__ void copy_probe(const float4* __restrict__ in, float4* __restrict__ out, size_t n_in, size_t n_out) {
+  const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
+  float4 acc = make_float4(0, 0, 0, 0);
+  for (size_t i = blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x; i < n_in; i += stride) {
+    const float4 x = in[i];
+    acc.x += x.x;
+    acc.y += x.y;
+    acc.z += x.z;
+    acc.w += x.w;
+    if (i < n_out) out[i] = x;
+  }
+  if (acc.x == 1234.5f) out[0] = acc;
+}
+
+int main() {
+  const int kB = 3;
+  const size_t n_in = static_cast<size_t>(kB) * kRows * kL;
+  std::vector<float2> h_in(n_in);
+  uint32_t s = 12345;
+  for (auto& z : h_in) {
+    s = s * 1664525u + 1013904223u;
+    z.x = (s >> 8) * (1.0f / 16777216.0f) - 0.5f;
+    s = s * 1664525u + 1013904223u;
+    z.y = (s >> 8) * (1.0f / 16777216.0f) - 0.5f;
+  }
+  std::vector<float2> h_w(kL);
+  for (int e = 0; e < kL; ++e) {
+    const double a = -2.0 * M_PI * e / kL;
+    h_w[e] = make_float2(static_cast<float>(std::cos(a)), static_cast<float>(std::sin(a)));
+  }
+  float2 *d_in, *d_w;
+  float* d_out;
+  CHECK(hipMalloc(&d_in, n_in * sizeof(float2)));
+  CHECK(hipMalloc(&d_out, n_in * sizeof(float)));
+  CHECK(hipMalloc(&d_w, kL * sizeof(float2)));
+  CHECK(hipMemcpy(d_in, h_in.data(), n_in * sizeof(float2), hipMemcpyHostToDevice));
+  CHECK(hipMemcpy(d_w, h_w.data(), kL * sizeof(float2), hipMemcpyHostToDevice));
+
+  hipLaunchKernelGGL(rowfft16k, dim3(kRows, kB), dim3(kNT), 0, 0, d_in, d_out, d_w);
+  CHECK(hipGetLastError());
+  CHECK(hipDeviceSynchronize());
+  std::vector<float> h_out(n_in);
+  CHECK(hipMemcpy(h_out.data(), d_out, n_in * sizeof(float), hipMemcpyDeviceToHost));
+  // check rows against a double-precision DFT (power), a few bins per row
+  double worst = 0.0;
+  const int rows_chk[] = {0, 1, 200, 384, kRows + 7, 2 * kRows + 384};
+  for (int r : rows_chk) {
+    const float2* x = &h_in[static_cast<size_t>(r) * kL];
+    double scale = 0.0;
+    for (int k = 0; k < kL; k += 1) {
+      if (k % 97 != 0 && k > 40) continue;
+      double re = 0, im = 0;
+      for (int n = 0; n < kL; ++n) {
+        const double a = -2.0 * M_PI * static_cast<double>((static_cast<uint64_t>(n) * k) % kL) / kL;
+        re += x[n].x * std::cos(a) - x[n].y * std::sin(a);
+        im += x[n].x * std::sin(a) + x[n].y * std::cos(a);
+      }
+      const double p = re * re + im * im;
+      scale = std::max(scale, p);
+      const double got = h_out[static_cast<size_t>(r) * kL + k];
+      worst = std::max(worst, std::fabs(got - p) / std::max(p, 1.0));
+    }
+  }
+  std::printf("check: worst relative power error %.3e (%s)\n", worst, worst < 1e-4 ? "ok" : "FAIL");
+  if (!(worst < 1e-4)) return 1;
+
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  for (int nb : {1, 3}) {
+    const int reps = 50;
+    for (int i = 0; i < 3; ++i) hipLaunchKernelGGL(rowfft16k, dim3(kRows, nb), dim3(kNT), 0, 0, d_in, d_out, d_w);
+    CHECK(hipEventRecord(e0));
+    for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(rowfft16k, dim3(kRows, nb), dim3(kNT), 0, 0, d_in, d_out, d_w);
+    CHECK(hipEventRecord(e1));
+    CHECK(hipEventSynchronize(e1));
+    float ms;
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    std::printf("rowfft16k  %d template(s) per launch: %8.2f us per template\n", nb, 1e3 * ms / reps / nb);
+    const size_t n4 = static_cast<size_t>(nb) * kRows * kL / 2, n4o = n4 / 2;
+    for (int i = 0; i < 3; ++i)
+      hipLaunchKernelGGL(copy_probe, dim3(4096), dim3(256), 0, 0, reinterpret_cast<const float4*>(d_in),
+                         reinterpret_cast<float4*>(d_out), n4, n4o);
+    CHECK(hipEventRecord(e0));
+    for (int i = 0; i < reps; ++i)
+      hipLaunchKernelGGL(copy_probe, dim3(4096), dim3(256), 0, 0, reinterpret_cast<const float4*>(d_in),
+                         reinterpret_cast<float4*>(d_out), n4, n4o);
+    CHECK(hipEventRecord(e1));
+    CHECK(hipEventSynchronize(e1));
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    std::printf("copy       %d template(s) per launch: %8.2f us per template (same bytes)\n", nb,
+                1e3 * ms / reps / nb);
+    // pass A shape: the 16 MB series (one 2^22-sample work unit) -> 50.5 MB of rows
+    const float* series = reinterpret_cast<const float*>(d_out);
+    for (int i = 0; i < 3; ++i)
+      hipLaunchKernelGGL(passA_shape, dim3(kL / 16, nb), dim3(256), 0, 0, series, d_in);
+    CHECK(hipEventRecord(e0));
+    for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(passA_shape, dim3(kL / 16, nb), dim3(256), 0, 0, series, d_in);
+    CHECK(hipEventRecord(e1));
+    CHECK(hipEventSynchronize(e1));
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    std::printf("passA_shape %d template(s) per launch: %8.2f us per template (16 MB gather, 50.5 MB rows)\n", nb,
+                1e3 * ms / reps / nb);
+  }
+  CHECK(hipGetLastError());
+  return 0;
+}
