@@ -182,6 +182,79 @@ __global__ void __launch_bounds__(kNT) rowfft16k(const float2* __restrict__ in, 
   }
 }
 
+
+// 8192-point rows (N = 1536 x 8192: 769 rows), 512 threads x 16 points, radix
+// 16 | 16 | 16 | 2 (the last across lane pairs), 68 KB LDS: two workgroups per CU
+constexpr int kL8 = 8192, kRows8 = 769, kNT8 = 512;
+__device__ __forceinline__ int pidx8(int a) { return a + 2 * (a >> 5); }
+__global__ void __launch_bounds__(kNT8) rowfft8k(const float2* __restrict__ in, float* __restrict__ out,
+                                                 const float2* __restrict__ w16k) {
+  __shared__ float2 lds[kL8 + 2 * (kL8 / 32)];
+  __shared__ float2 t512[512], thi[64], tlo[128];  // W_512^e, W_8192^{128 e}, W_8192^e
+  t512[threadIdx.x] = w16k[32 * threadIdx.x];
+  if (threadIdx.x < 64) thi[threadIdx.x] = w16k[256 * threadIdx.x];
+  if (threadIdx.x < 128) tlo[threadIdx.x] = w16k[2 * threadIdx.x];
+  __syncthreads();
+  const int row = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
+  const float2* src = in + (static_cast<size_t>(b) * kRows8 + row) * kL8;
+  float2 v[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) v[q] = src[t + 512 * q];
+  dft16(v);
+#pragma unroll
+  for (int k = 1; k < 16; ++k) {
+    const int e = (t * k) & (kL8 - 1);
+    v[k] = cmul(v[k], cmul(thi[e >> 7], tlo[e & 127]));
+  }
+#pragma unroll
+  for (int k = 0; k < 16; ++k) lds[pidx8(k * 512 + t)] = v[k];
+  __syncthreads();
+  {
+    const int k0 = t >> 5, t1 = t & 31;
+    const int base = k0 * 512 + t1;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) v[q] = lds[pidx8(base + 32 * q)];
+    dft16(v);
+#pragma unroll
+    for (int k = 1; k < 16; ++k) v[k] = cmul(v[k], t512[(t1 * k) & 511]);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) lds[pidx8(base + 32 * k)] = v[k];
+  }
+  __syncthreads();
+  const int t2 = t & 1, k1 = (t >> 1) & 15, k0 = t >> 5;
+  {
+    const int base = k0 * 512 + k1 * 32 + t2;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) v[q] = lds[pidx8(base + 2 * q)];
+    dft16(v);
+#pragma unroll
+    for (int k = 1; k < 16; ++k) v[k] = cmul(v[k], t512[(16 * t2 * k) & 511]);
+  }
+  // radix 2 across the lane pair: lane t2 ends with k3 = t2
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    float2 p;
+    p.x = __shfl_xor(v[k].x, 1);
+    p.y = __shfl_xor(v[k].y, 1);
+    v[k] = t2 ? csub(p, v[k]) : cadd(v[k], p);
+  }
+  __syncthreads();
+  float* pw = reinterpret_cast<float*>(lds);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int K = k0 + 16 * k1 + 256 * k + 4096 * t2;
+    pw[fidx(K)] = v[k].x * v[k].x + v[k].y * v[k].y;
+  }
+  __syncthreads();
+  float* dst = out + (static_cast<size_t>(b) * kRows8 + row) * kL8;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int K = 4 * t + 2048 * j;
+    const float4 o = make_float4(pw[fidx(K)], pw[fidx(K + 1)], pw[fidx(K + 2)], pw[fidx(K + 3)]);
+    reinterpret_cast<float4*>(dst)[K / 4] = o;
+  }
+}
+
 // memory shape of pass A (no arithmetic): a workgroup of 256 threads owns 16
 // adjacent columns n2; each thread reads the 16 samples of its 8 packed rows
 // (x[(2 m) 16384 + n2], x[(2 m + 1) 16384 + n2], m = tj + 16 q) and the
@@ -274,6 +347,30 @@ int main() {
   std::printf("check: worst relative power error %.3e (%s)\n", worst, worst < 1e-4 ? "ok" : "FAIL");
   if (!(worst < 1e-4)) return 1;
 
+
+  {
+    hipLaunchKernelGGL(rowfft8k, dim3(kRows8, 1), dim3(kNT8), 0, 0, d_in, d_out, d_w);
+    CHECK(hipDeviceSynchronize());
+    std::vector<float> o8(static_cast<size_t>(kRows8) * kL8);
+    CHECK(hipMemcpy(o8.data(), d_out, o8.size() * sizeof(float), hipMemcpyDeviceToHost));
+    double w8 = 0.0;
+    for (int r : {0, 5, 768}) {
+      const float2* x = &h_in[static_cast<size_t>(r) * kL8];
+      for (int k = 0; k < kL8; ++k) {
+        if (k % 89 != 0 && k > 20) continue;
+        double re = 0, im = 0;
+        for (int n = 0; n < kL8; ++n) {
+          const double a = -2.0 * M_PI * static_cast<double>((static_cast<uint64_t>(n) * k) % kL8) / kL8;
+          re += x[n].x * std::cos(a) - x[n].y * std::sin(a);
+          im += x[n].x * std::sin(a) + x[n].y * std::cos(a);
+        }
+        const double p = re * re + im * im;
+        w8 = std::max(w8, std::fabs(o8[static_cast<size_t>(r) * kL8 + k] - p) / std::max(p, 1.0));
+      }
+    }
+    std::printf("check 8k: worst relative power error %.3e (%s)\n", w8, w8 < 1e-4 ? "ok" : "FAIL");
+    if (!(w8 < 1e-4)) return 1;
+  }
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
@@ -287,6 +384,14 @@ int main() {
     float ms;
     CHECK(hipEventElapsedTime(&ms, e0, e1));
     std::printf("rowfft16k  %d template(s) per launch: %8.2f us per template\n", nb, 1e3 * ms / reps / nb);
+
+    for (int i = 0; i < 3; ++i) hipLaunchKernelGGL(rowfft8k, dim3(kRows8, nb), dim3(kNT8), 0, 0, d_in, d_out, d_w);
+    CHECK(hipEventRecord(e0));
+    for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(rowfft8k, dim3(kRows8, nb), dim3(kNT8), 0, 0, d_in, d_out, d_w);
+    CHECK(hipEventRecord(e1));
+    CHECK(hipEventSynchronize(e1));
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    std::printf("rowfft8k   %d template(s) per launch: %8.2f us per template (769 rows of 8192)\n", nb, 1e3 * ms / reps / nb);
     const size_t n4 = static_cast<size_t>(nb) * kRows * kL / 2, n4o = n4 / 2;
     for (int i = 0; i < 3; ++i)
       hipLaunchKernelGGL(copy_probe, dim3(4096), dim3(256), 0, 0, reinterpret_cast<const float4*>(d_in),
