@@ -10,6 +10,9 @@
 #include "search.hpp"
 
 int main(int argc, char** argv) {
+  // first: the parent (the PID the client waits for) leaves as soon as the
+  // child's results are on disk, not after the GPU context's teardown
+  brp::boinc::supervise();
   brp::trace::phase("main");
   brp::log_message(brp::LOG_INFO, true, "Application startup - thank you for supporting Einstein@Home!\n");
   brp::log_message(brp::LOG_DEBUG, true, "Setting up diagnotics and exception handling...\n");

@@ -1,13 +1,18 @@
 #include "runtime.hpp"
 
 #include <fcntl.h>
+#include <signal.h>
 #include <sys/mman.h>
+#include <sys/prctl.h>
 #include <sys/resource.h>
 #include <sys/stat.h>
+#include <sys/wait.h>
 #include <unistd.h>
 
 #include <atomic>
+#include <cerrno>
 #include <chrono>
+#include <cstdint>
 #include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
@@ -17,6 +22,7 @@
 #include <sstream>
 #include <thread>
 
+#include "../core/fault.hpp"
 #include "../core/log.hpp"
 #include "../core/trace.hpp"
 #include "client_shm.hpp"
@@ -43,6 +49,27 @@ std::atomic<double> g_last_checkpoint{0.0};
 std::atomic<double> g_checkpoint_cpu{0.0};
 std::atomic<double> g_wss{0.0}, g_max_wss{0.0};
 std::atomic<int> g_status_sent{0};
+
+// supervise(): the child's end of the status pipe (-1: not supervised)
+int g_report_fd = -1;
+pid_t g_child = -1;
+
+// the exit status to the supervising parent (async-signal-safe; once)
+void report_status(int status) {
+  const int fd = g_report_fd;
+  if (fd < 0) return;
+  g_report_fd = -1;
+  const int32_t v = status;
+  ssize_t w;
+  do {
+    w = ::write(fd, &v, sizeof(v));
+  } while (w < 0 && errno == EINTR);
+  (void)w;
+}
+
+void forward_signal(int sig) {
+  if (g_child > 0) ::kill(g_child, sig);
+}
 
 std::mutex g_suspend_mu;
 std::condition_variable g_suspend_cv;
@@ -154,6 +181,7 @@ void wake_suspended() {
 [[noreturn]] void exit_now(int status) {
   std::fflush(nullptr);
   if (g_lock_fd >= 0) ::close(g_lock_fd);
+  report_status(status);
   _exit(status);
 }
 
@@ -382,7 +410,12 @@ void finish(int status) {
   // results, checkpoint removal and the finish marker are on disk: leave
   // without the HIP runtime's and the C++ statics' teardown (the kernel driver
   // reclaims device memory at process exit); BRP_FAST_EXIT=0 keeps exit()
-  if (fast_exit_enabled()) ::_exit(status);
+  if (fast_exit_enabled()) {
+    report_status(status);
+    std::string ms;
+    if (fault_enabled("slow_exit", &ms)) std::this_thread::sleep_for(std::chrono::milliseconds(std::atol(ms.c_str())));
+    ::_exit(status);
+  }
   std::exit(status);
 }
 
@@ -419,7 +452,68 @@ void finish_from_signal(int status) {
     (void)w;
     ::close(fd);
   }
+  report_status(status);
   _exit(status);
+}
+
+void supervise() {
+#if defined(__SANITIZE_ADDRESS__) || defined(__SANITIZE_THREAD__)
+  return;
+#elif defined(__has_feature)
+#if __has_feature(address_sanitizer) || __has_feature(thread_sanitizer)
+  return;
+#endif
+#endif
+  const char* e = std::getenv("BRP_SUPERVISE");
+  if (e && std::strcmp(e, "0") == 0) return;
+  int fds[2];
+  if (::pipe2(fds, O_CLOEXEC) != 0) return;  // run unsupervised
+  std::fflush(nullptr);
+  const pid_t parent = ::getpid();
+  const pid_t pid = ::fork();
+  if (pid < 0) {
+    ::close(fds[0]);
+    ::close(fds[1]);
+    return;
+  }
+  if (pid == 0) {
+    ::close(fds[0]);
+    g_report_fd = fds[1];
+    // the client's SIGKILL of the parent takes the child (and its GPU work) with it
+    ::prctl(PR_SET_PDEATHSIG, SIGKILL);
+    if (::getppid() != parent) _exit(kExitAbortedByClient);
+    return;
+  }
+  ::close(fds[1]);
+  g_child = pid;
+  struct sigaction sa{};
+  sa.sa_handler = forward_signal;
+  sigemptyset(&sa.sa_mask);
+  sa.sa_flags = SA_RESTART;
+  for (int sig : {SIGTERM, SIGINT, SIGHUP, SIGQUIT, SIGUSR1, SIGUSR2, SIGCONT}) ::sigaction(sig, &sa, nullptr);
+  int32_t v = 0;
+  size_t got = 0;
+  while (got < sizeof(v)) {
+    const ssize_t r = ::read(fds[0], reinterpret_cast<char*>(&v) + got, sizeof(v) - got);
+    if (r > 0) got += static_cast<size_t>(r);
+    else if (r < 0 && errno == EINTR) continue;
+    else break;  // EOF: the child left without reporting
+  }
+  if (got == sizeof(v)) _exit(v);  // results on disk; the child's teardown goes on without us
+  int st = 0;
+  while (::waitpid(pid, &st, 0) < 0 && errno == EINTR) {
+  }
+  if (WIFEXITED(st)) _exit(WEXITSTATUS(st));
+  if (WIFSIGNALED(st)) {
+    const int sig = WTERMSIG(st);
+    struct sigaction dfl{};
+    dfl.sa_handler = SIG_DFL;
+    sigemptyset(&dfl.sa_mask);
+    ::sigaction(sig, &dfl, nullptr);
+    ::raise(sig);
+    _exit(128 + sig);
+  }
+  _exit(1);
 }
 
 }  // namespace boinc

@@ -103,5 +103,19 @@ bool fast_exit_enabled();
 // async-signal-safe finish for fatal signal handlers (open/write/_exit only)
 [[noreturn]] void finish_from_signal(int status);
 
+// Process supervision (the app binary's first call, before any thread or HIP
+// call): the process forks; the child returns and runs the application, the
+// parent -- the PID the BOINC client and /usr/bin/time wait for -- waits for
+// it and never touches the GPU. Every exit path of the child reports its
+// status once the results and markers are on disk (finish, quit, temporary
+// exit, fatal signals), and the parent leaves with that status at once: the
+// kernel driver's teardown of the child's GPU context (80-120 ms on MI355X,
+// profiles/app_phases_r6.txt) no longer delays the client. A child that dies
+// without reporting is waited for and its status or signal mirrored.
+// Termination signals sent to the parent are forwarded to the child, and the
+// child is killed if the parent dies (SIGKILL from the client). Off with
+// BRP_SUPERVISE=0 and in sanitizer builds.
+void supervise();
+
 }  // namespace boinc
 }  // namespace brp

@@ -15,6 +15,9 @@
 //   slow_template:MS       sleep MS ms per applied template (paces client tests)
 //   resource_error         the search returns a host allocation failure
 //                          (-> BOINC temporary exit)
+//   slow_exit:MS           finish() sleeps MS ms after reporting its status to the
+//                          supervising parent (stands in for the GPU context's
+//                          teardown in CPU tests of boinc::supervise)
 //   collective_timeout[:R] rank R (default 1) stalls before the all-gather
 //                          (Python side, parallel/dist.py)
 #pragma once

@@ -256,3 +256,94 @@ def test_tsan_under_client_suspend_resume_quit(case, reference_result, tmp_path)
         cl2.close()
     assert rc == 0 and "ThreadSanitizer" not in err, err[-6000:]
     assert _cands(slot / "result.cand") == reference_result
+
+
+def _children(pid):
+    try:
+        return [int(x) for x in Path(f"/proc/{pid}/task/{pid}/children").read_text().split()]
+    except OSError:
+        return []
+
+
+def _alive(pid):
+    try:
+        st = Path(f"/proc/{pid}/stat").read_text().split(") ")[-1].split()[0]
+    except OSError:
+        return False
+    return st != "Z"
+
+
+def test_supervised_run_equals_unsupervised(app, case, reference_result, tmp_path):
+    """BRP_SUPERVISE (default on): the parent the client waits for leaves with
+    the child's status; results, markers and exit codes are those of an
+    unsupervised run (BRP_SUPERVISE=0)."""
+    for sup in ("1", "0"):
+        d = tmp_path / f"sup{sup}"
+        d.mkdir()
+        r = subprocess.run([str(a) for a in _args(app, case)], cwd=d, capture_output=True, text=True, timeout=300,
+                           env=dict(os.environ, BRP_SUPERVISE=sup))
+        assert r.returncode == 0, r.stderr[-2000:]
+        assert _cands(d / "result.cand") == reference_result
+        assert (d / "boinc_finish_called").read_text().strip() == "0"
+    # a fatal signal in the worker: same exit status either way
+    codes = []
+    for sup in ("1", "0"):
+        d = tmp_path / f"segv{sup}"
+        d.mkdir()
+        r = subprocess.run([str(a) for a in _args(app, case)], cwd=d, capture_output=True, text=True, timeout=300,
+                           env=dict(os.environ, BRP_SUPERVISE=sup, BRP_FAULT="segv_after_template:3",
+                                    BRP_CRASH_SLEEP="0"))
+        codes.append(r.returncode)
+    assert codes[0] == codes[1] == signal.SIGSEGV
+
+
+def test_supervisor_parent_death_kills_child(app, case, tmp_path):
+    """SIGKILL of the parent (the client's hard kill) takes the worker child
+    with it (PR_SET_PDEATHSIG): no orphan keeps the GPU."""
+    p = subprocess.Popen([str(a) for a in _args(app, case)], cwd=tmp_path, stdout=subprocess.DEVNULL,
+                         stderr=subprocess.DEVNULL, env=dict(os.environ, **_slow_env()))
+    try:
+        kids = []
+        for _ in range(100):
+            kids = _children(p.pid)
+            if kids:
+                break
+            time.sleep(0.05)
+        assert len(kids) == 1, "the supervised app runs its work in one child"
+        child = kids[0]
+        time.sleep(0.5)
+        assert _alive(child)
+        p.kill()
+        p.wait(timeout=10)
+        for _ in range(100):
+            if not _alive(child):
+                break
+            time.sleep(0.05)
+        assert not _alive(child), "worker child survived its parent"
+    finally:
+        if p.poll() is None:
+            p.kill()
+            p.wait()
+
+
+def test_supervisor_parent_leaves_before_child_teardown(app, case, tmp_path):
+    """The parent exits once the child has reported (results and the finish
+    marker on disk), not when the child is gone: BRP_FAULT=slow_exit holds the
+    child 3 s after its report, as the GPU context's teardown does for ~0.1 s
+    (the parent's exit then ends the delay: PR_SET_PDEATHSIG)."""
+    t0 = time.perf_counter()
+    p = subprocess.Popen([str(a) for a in _args(app, case)], cwd=tmp_path, stdout=subprocess.DEVNULL,
+                         stderr=subprocess.DEVNULL, env=dict(os.environ, BRP_FAULT="slow_exit:3000"))
+    rc = p.wait(timeout=120)
+    t_parent = time.perf_counter() - t0
+    assert rc == 0
+    assert (tmp_path / "boinc_finish_called").read_text().strip() == "0"
+    assert _cands(tmp_path / "result.cand")
+    # unsupervised, the same run waits for the delay
+    d = tmp_path / "unsup"
+    d.mkdir()
+    t1 = time.perf_counter()
+    r = subprocess.run([str(a) for a in _args(app, case)], cwd=d, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
+                       env=dict(os.environ, BRP_FAULT="slow_exit:3000", BRP_SUPERVISE="0"), timeout=120)
+    assert r.returncode == 0
+    assert time.perf_counter() - t1 >= 3.0 > t_parent + 1.0
