@@ -3,8 +3,9 @@
 A from-scratch re-design of the capabilities of boinc-app-eah-brp for AMD
 Instinct MI355X (gfx950): the per-template pipeline (time-domain resampling,
 3*2^n-point real FFT + power spectrum, 16-harmonic summing, candidate
-selection) runs as hand-written HIP kernels, templates are batched in HBM and
-replayed through HIP graphs, and template banks are sharded over GPUs with
+selection) runs as hand-written HIP kernels, templates stream through three
+pipelines (HIP streams) per GPU with two batches in flight each (HIP graph
+replay optional, BRP_GRAPH=1), and template banks are sharded over GPUs with
 RCCL all-gathers of the candidate tables.
 
 Layout:
