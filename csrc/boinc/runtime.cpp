@@ -67,8 +67,11 @@ void report_status(int status) {
   (void)w;
 }
 
-void forward_signal(int sig) {
-  if (g_child > 0) ::kill(g_child, sig);
+// a signal sent to the parent's PID goes on to the child; one the terminal
+// sent to the whole foreground process group (Ctrl-C: SI_KERNEL) reached the
+// child already and is not doubled (the crash handler counts kill signals)
+void forward_signal(int sig, siginfo_t* info, void*) {
+  if (g_child > 0 && (info == nullptr || info->si_code != SI_KERNEL)) ::kill(g_child, sig);
 }
 
 std::mutex g_suspend_mu;
@@ -487,9 +490,9 @@ void supervise() {
   ::close(fds[1]);
   g_child = pid;
   struct sigaction sa{};
-  sa.sa_handler = forward_signal;
+  sa.sa_sigaction = forward_signal;
   sigemptyset(&sa.sa_mask);
-  sa.sa_flags = SA_RESTART;
+  sa.sa_flags = SA_RESTART | SA_SIGINFO;
   for (int sig : {SIGTERM, SIGINT, SIGHUP, SIGQUIT, SIGUSR1, SIGUSR2, SIGCONT}) ::sigaction(sig, &sa, nullptr);
   int32_t v = 0;
   size_t got = 0;
